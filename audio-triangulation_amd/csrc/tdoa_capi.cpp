@@ -1,0 +1,616 @@
+// tdoa_capi.cpp -- host side of libtdoa: configuration, one-time tables and
+// the batched entry points declared in include/tdoa.h.
+//
+// The one-time tables reproduce the reference's float arithmetic exactly and
+// are therefore built on the host (this file is compiled with
+// -ffp-contract=off, no fast-math):
+//   microphones_init      src/components/microphones.c:9-33
+//   per-cell lag LUT      src/components/vga/vga_heatmap.h:48-93
+//   Gaussian lag prior    src/components/correlations.c:26-33 (exp in libm)
+//   DPSS(N, 2) Q15 window window.ipynb cells 2-4 (scipy dpss procedure)
+// Everything per frame runs in the gfx950 kernels (tdoa_kernels.hip).
+
+#include "../../include/tdoa.h"
+#include "tdoa_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess)                                                  \
+            return fail(TDOA_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int ilog2(int n)
+{
+    int b = 0;
+    while ((1 << b) < n)
+        b++;
+    return b;
+}
+
+// ---------------------------------------------------------------- DPSS
+// First Slepian taper of length n and time-bandwidth nw: the eigenvector of
+// the largest eigenvalue of the symmetric tridiagonal matrix
+//   diag_i = ((n-1-2i)/2)^2 cos(2 pi nw/n),  off_i = i(n-i)/2
+// (Percival & Walden 1993, the system scipy.signal.windows.dpss solves).
+// Largest eigenvalue by Sturm-count bisection, vector by inverse iteration
+// with a partially pivoted tridiagonal LU.
+int sturm_count_below(const std::vector<double> &d, const std::vector<double> &e2, double x)
+{
+    int cnt = 0;
+    double q = d[0] - x;
+    if (q < 0)
+        cnt++;
+    for (size_t i = 1; i < d.size(); i++) {
+        if (q == 0.0)
+            q = 1e-300;
+        q = d[i] - x - e2[i] / q;
+        if (q < 0)
+            cnt++;
+    }
+    return cnt;
+}
+
+void tridiag_solve_pivoted(const std::vector<double> &d, const std::vector<double> &e,
+                           double lam, std::vector<double> &b)
+{
+    // Solve (T - lam I) x = b in place; e[i] couples rows i-1 and i (e[0] unused).
+    const int n = (int)d.size();
+    std::vector<double> a(n), c(n), u2(n, 0.0), l(n, 0.0), dd(n);
+    std::vector<int> piv(n, 0);
+    // rows: sub a_i = e[i] (i>=1), diag dd_i = d_i - lam, super c_i = e[i+1]
+    for (int i = 0; i < n; i++) {
+        dd[i] = d[i] - lam;
+        a[i] = i > 0 ? e[i] : 0.0;
+        c[i] = i + 1 < n ? e[i + 1] : 0.0;
+    }
+    // Gaussian elimination with partial pivoting (LAPACK dgttrf style)
+    for (int i = 0; i < n - 1; i++) {
+        if (std::fabs(dd[i]) >= std::fabs(a[i + 1])) {
+            double f = dd[i] != 0.0 ? a[i + 1] / dd[i] : 0.0;
+            if (dd[i] == 0.0)
+                dd[i] = 1e-300;
+            l[i] = f;
+            dd[i + 1] -= f * c[i];
+            b[i + 1] -= f * b[i];
+            u2[i] = 0.0;
+            piv[i] = 0;
+        } else {
+            double f = dd[i] / a[i + 1];
+            l[i] = f;
+            // swap rows i and i+1
+            double t_d = a[i + 1], t_c = dd[i + 1], t_u2 = i + 2 < n ? c[i + 1] : 0.0;
+            double nd1 = c[i] - f * t_c;
+            double nu2 = -f * t_u2;
+            dd[i] = t_d;
+            c[i] = t_c;
+            u2[i] = t_u2;
+            dd[i + 1] = nd1;
+            if (i + 2 < n)
+                c[i + 1] = nu2;
+            double tb = b[i];
+            b[i] = b[i + 1];
+            b[i + 1] = tb - f * b[i];
+            piv[i] = 1;
+        }
+    }
+    if (dd[n - 1] == 0.0)
+        dd[n - 1] = 1e-300;
+    // back substitution
+    b[n - 1] /= dd[n - 1];
+    if (n > 1)
+        b[n - 2] = (b[n - 2] - c[n - 2] * b[n - 1]) / dd[n - 2];
+    for (int i = n - 3; i >= 0; i--)
+        b[i] = (b[i] - c[i] * b[i + 1] - u2[i] * b[i + 2]) / dd[i];
+}
+
+}  // namespace
+
+extern "C" int tdoa_dpss_q15(int32_t n, double nw, int32_t *out)
+{
+    if (n < 4 || !out || !(nw > 0))
+        return fail(TDOA_ERR_INVALID, "tdoa_dpss_q15: bad arguments");
+    const double W = nw / n, cw = std::cos(2.0 * M_PI * W);
+    std::vector<double> d(n), e(n, 0.0), e2(n, 0.0);
+    for (int i = 0; i < n; i++) {
+        const double t = (n - 1 - 2.0 * i) / 2.0;
+        d[i] = t * t * cw;
+    }
+    for (int i = 1; i < n; i++) {
+        e[i] = i * (double)(n - i) / 2.0;
+        e2[i] = e[i] * e[i];
+    }
+    // Gershgorin bounds
+    double lo = 1e300, hi = -1e300;
+    for (int i = 0; i < n; i++) {
+        double r = std::fabs(e[i]) + (i + 1 < n ? std::fabs(e[i + 1]) : 0.0);
+        lo = std::min(lo, d[i] - r);
+        hi = std::max(hi, d[i] + r);
+    }
+    // largest eigenvalue: smallest x with count_below(x) == n
+    for (int it = 0; it < 200; it++) {
+        double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi)
+            break;
+        if (sturm_count_below(d, e2, mid) >= n)
+            hi = mid;
+        else
+            lo = mid;
+    }
+    const double lam = 0.5 * (lo + hi);
+    std::vector<double> v(n, 1.0);
+    for (int it = 0; it < 4; it++) {
+        tridiag_solve_pivoted(d, e, lam, v);
+        double nrm = 0;
+        for (double x : v)
+            nrm += x * x;
+        nrm = std::sqrt(nrm);
+        for (double &x : v)
+            x /= nrm;
+    }
+    double s = 0, mx = 0;
+    for (double x : v)
+        s += x;
+    if (s < 0)
+        for (double &x : v)
+            x = -x;
+    for (double x : v)
+        mx = std::max(mx, std::fabs(x));
+    for (int i = 0; i < n; i++)
+        out[i] = (int32_t)std::nearbyint(v[i] / mx * 32767.0);
+    return TDOA_OK;
+}
+
+// ------------------------------------------------------------ context
+struct tdoa_ctx {
+    tdoa_config cfg;
+    int device;
+    int M, N, P, K, S, G, W, H, U, TW;
+    std::vector<float> mic;     // [M][2]
+    std::vector<int32_t> win;   // [N]
+    std::vector<float> prior;   // [K]
+    std::vector<uint8_t> lut;   // [P][G]
+    std::vector<uint32_t> tuples;
+    std::vector<int32_t> tuple_cell;
+    // device
+    int16_t *d_window = nullptr;
+    float *d_prior = nullptr;
+    uint32_t *d_tuples = nullptr;
+    int32_t *d_tuple_cell = nullptr;
+    tdoa_kparams kp;
+};
+
+namespace {
+
+// microphones.c:9-33 (constants.h:17-19: AB .132, BC .15, CA .20; MIRROR on)
+void reference_triangle(float *xy)
+{
+    const float dAB = 0.132f, dBC = 0.15f, dCA = 0.20f;
+    const float xC = (dAB * dAB + dCA * dCA - dBC * dBC) / (2.0f * dAB);
+    const float yC = sqrtf(fmaxf(0.0f, dCA * dCA - xC * xC));
+    const float pAx = 0.0f, pAy = 0.0f, pBx = dAB, pBy = 0.0f;
+    const float pCx = xC, pCy = yC * -1.0f;
+    const float cx = (pAx + pBx + pCx) / 3.0f;
+    const float cy = (pAy + pBy + pCy) / 3.0f;
+    xy[0] = pAx - cx;
+    xy[1] = pAy - cy;
+    xy[2] = pBx - cx;
+    xy[3] = pBy - cy;
+    xy[4] = pCx - cx;
+    xy[5] = pCy - cy;
+}
+
+inline float hypot3(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
+// vga_heatmap.h:48-93, generalised to lexicographic pairs of M mics.
+void build_lut(tdoa_ctx *c)
+{
+    const int W = c->W, H = c->H, G = c->G;
+    const float scale = c->cfg.grid_scale, hgt = c->cfg.height_offset;
+    const float sos = c->cfg.speed_of_sound;
+    const int fs = c->cfg.sample_rate_hz;
+    c->lut.assign((size_t)c->P * G, 0);
+    std::vector<float> d(c->M);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float xm = (float)(x - c->cfg.grid_half_w) / scale;
+            float ym = (float)(c->cfg.grid_half_h - y) / scale;
+            float zm = hgt;
+            const float k = hgt / hypot3(zm, xm, ym);
+            xm *= k;
+            ym *= k;
+            zm *= k;
+            for (int m = 0; m < c->M; m++)
+                d[m] = hypot3(zm, xm - c->mic[2 * m], ym - c->mic[2 * m + 1]);
+            int p = 0;
+            for (int i = 0; i < c->M; i++)
+                for (int j = i + 1; j < c->M; j++, p++) {
+                    const float dt = (d[j] - d[i]) / sos;
+                    int s = (int)roundf(dt * (float)fs);
+                    s = std::min(std::max(s, -c->S), c->S);
+                    c->lut[(size_t)p * G + (size_t)y * W + x] = (uint8_t)(s + c->S);
+                }
+        }
+    // Distinct lag tuples in order of their first (row-major) cell: the max
+    // over cells equals the max over tuples, and the first argmax tuple
+    // carries the first argmax cell (tuple first-cells are increasing).
+    std::map<std::vector<uint8_t>, int> seen;
+    c->tuples.clear();
+    c->tuple_cell.clear();
+    std::vector<uint8_t> key(c->P);
+    for (int cell = 0; cell < G; cell++) {
+        for (int p = 0; p < c->P; p++)
+            key[p] = c->lut[(size_t)p * G + cell];
+        if (seen.emplace(key, (int)c->tuple_cell.size()).second) {
+            c->tuple_cell.push_back(cell);
+            for (int w = 0; w < c->TW; w++) {
+                uint32_t v = 0;
+                for (int b = 0; b < 4; b++) {
+                    int p = 4 * w + b;
+                    if (p < c->P)
+                        v |= (uint32_t)key[p] << (8 * b);
+                }
+                c->tuples.push_back(v);
+            }
+        }
+    }
+    c->U = (int)c->tuple_cell.size();
+}
+
+void free_device(tdoa_ctx *c)
+{
+    (void)hipFree(c->d_window);
+    (void)hipFree(c->d_prior);
+    (void)hipFree(c->d_tuples);
+    (void)hipFree(c->d_tuple_cell);
+    c->d_window = nullptr;
+    c->d_prior = nullptr;
+    c->d_tuples = nullptr;
+    c->d_tuple_cell = nullptr;
+}
+
+}  // namespace
+
+extern "C" int tdoa_config_default(tdoa_config *cfg)
+{
+    if (!cfg)
+        return fail(TDOA_ERR_INVALID, "tdoa_config_default: NULL");
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->num_mics = 3;
+    cfg->frame_len = 1024;
+    cfg->sample_rate_hz = 50000;
+    cfg->max_shift = 0;
+    cfg->speed_of_sound = 343.0f;
+    cfg->engine = TDOA_ENGINE_DIRECT;
+    cfg->mic_xy = nullptr;
+    cfg->grid_half_w = 50;
+    cfg->grid_half_h = 50;
+    cfg->grid_scale = 24.0f;
+    cfg->height_offset = 1.2f;
+    cfg->window_q15 = nullptr;
+    cfg->phat_eps = 1e-20f;
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
+{
+    if (!cfg || !out)
+        return fail(TDOA_ERR_INVALID, "tdoa_create: NULL argument");
+    *out = nullptr;
+    const int M = cfg->num_mics, N = cfg->frame_len;
+    if (M < 2 || M > TDOA_MAX_MICS)
+        return fail(TDOA_ERR_INVALID, "num_mics %d outside [2,%d]", M, TDOA_MAX_MICS);
+    if (N < 256 || N > 4096 || (N & (N - 1)))
+        return fail(TDOA_ERR_INVALID, "frame_len %d must be a power of two in [256,4096]", N);
+    if (cfg->sample_rate_hz <= 0 || !(cfg->speed_of_sound > 0))
+        return fail(TDOA_ERR_INVALID, "sample_rate_hz / speed_of_sound must be positive");
+    // constants.h:12 -- SAMPLE_RATE_HZ * 32 / 34300 (integer division)
+    const int S = cfg->max_shift > 0 ? cfg->max_shift
+                                     : (int)((int64_t)cfg->sample_rate_hz * 32 / 34300);
+    if (S < 1 || S > 63)
+        return fail(TDOA_ERR_INVALID, "max_shift %d outside [1,63]", S);
+    if (cfg->engine != TDOA_ENGINE_DIRECT && cfg->engine != TDOA_ENGINE_GCC_PHAT)
+        return fail(TDOA_ERR_INVALID, "unknown engine %d", cfg->engine);
+    if (cfg->grid_half_w < 0 || cfg->grid_half_h < 0 || cfg->grid_half_w > 1000 ||
+        cfg->grid_half_h > 1000 || !(cfg->grid_scale > 0) || !(cfg->height_offset > 0))
+        return fail(TDOA_ERR_INVALID, "bad grid geometry");
+    if (M != 3 && !cfg->mic_xy)
+        return fail(TDOA_ERR_INVALID, "mic_xy is required unless num_mics == 3");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(TDOA_ERR_NO_DEVICE, "no HIP device visible (libtdoa has no CPU path)");
+    if (device < 0 || device >= ndev)
+        return fail(TDOA_ERR_INVALID, "device %d out of range (%d visible)", device, ndev);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(TDOA_ERR_NO_DEVICE, "device %d is %s; libtdoa is built for gfx950 only",
+                    device, prop.gcnArchName);
+
+    tdoa_ctx *c = new tdoa_ctx();
+    c->cfg = *cfg;
+    c->cfg.mic_xy = nullptr;
+    c->cfg.window_q15 = nullptr;
+    c->cfg.max_shift = S;
+    c->device = device;
+    c->M = M;
+    c->N = N;
+    c->P = M * (M - 1) / 2;
+    c->S = S;
+    c->K = 2 * S + 1;
+    c->W = 2 * cfg->grid_half_w + 1;
+    c->H = 2 * cfg->grid_half_h + 1;
+    c->G = c->W * c->H;
+    c->TW = (c->P + 3) / 4;
+
+    c->mic.resize(2 * M);
+    if (cfg->mic_xy)
+        std::memcpy(c->mic.data(), cfg->mic_xy, sizeof(float) * 2 * M);
+    else
+        reference_triangle(c->mic.data());
+
+    c->win.resize(N);
+    if (cfg->window_q15) {
+        for (int i = 0; i < N; i++) {
+            if (cfg->window_q15[i] < 0 || cfg->window_q15[i] > 32767) {
+                delete c;
+                return fail(TDOA_ERR_INVALID, "window_q15[%d] outside [0,32767]", i);
+            }
+            c->win[i] = cfg->window_q15[i];
+        }
+    } else {
+        int rc = tdoa_dpss_q15(N, 2.0, c->win.data());
+        if (rc) {
+            delete c;
+            return rc;
+        }
+    }
+
+    // correlations.c:27-30: scale = (float)exp((double)((float)(-d^2) / 36.f))
+    c->prior.resize(c->K);
+    for (int d = 0; d < c->K; d++) {
+        const float arg = (float)(-(d * d)) / 36.f;
+        c->prior[d] = (float)std::exp((double)arg);
+    }
+
+    build_lut(c);
+
+    // kernel parameters
+    tdoa_kparams &kp = c->kp;
+    std::memset(&kp, 0, sizeof kp);
+    kp.M = M;
+    kp.N = N;
+    kp.log2N = ilog2(N);
+    kp.P = c->P;
+    kp.K = c->K;
+    kp.S = S;
+    kp.G = c->G;
+    kp.U = c->U;
+    kp.grid_W = c->W;
+    kp.half_w = cfg->grid_half_w;
+    kp.half_h = cfg->grid_half_h;
+    kp.grid_scale = cfg->grid_scale;
+    kp.sbase = (S % 2 == 0) ? -S : -S - 1;
+    kp.T = (S - kp.sbase + 1 + TDOA_LT - 1) / TDOA_LT;
+    kp.NSEG = (N / 2) / TDOA_SEGW;
+    // rows are read at word offsets [h, h + SEGW*NSEG + LT2 + 1) with
+    // h in [sbase/2, sbase/2 + LT2*(T-1)]
+    const int need_left = -kp.sbase / 2;
+    const int need_right = kp.sbase / 2 + TDOA_LT2 * (kp.T - 1) + TDOA_LT2 + 2;
+    kp.PADW = ((std::max(need_left, need_right) + 3) / 4) * 4;
+    kp.RS = N / 2 + 2 * kp.PADW;
+    kp.TW = c->TW;
+    {
+        int p = 0;
+        for (int i = 0; i < M; i++)
+            for (int j = i + 1; j < M; j++, p++) {
+                kp.pair_i[p] = (uint8_t)i;
+                kp.pair_j[p] = (uint8_t)j;
+            }
+    }
+
+    // upload
+    HIP_TRY(hipSetDevice(device));
+    std::vector<int16_t> w16(N);
+    for (int i = 0; i < N; i++)
+        w16[i] = (int16_t)c->win[i];
+    if (hipMalloc(&c->d_window, sizeof(int16_t) * N) != hipSuccess ||
+        hipMalloc(&c->d_prior, sizeof(float) * c->K) != hipSuccess ||
+        hipMalloc(&c->d_tuples, sizeof(uint32_t) * c->tuples.size()) != hipSuccess ||
+        hipMalloc(&c->d_tuple_cell, sizeof(int32_t) * c->U) != hipSuccess) {
+        free_device(c);
+        delete c;
+        return fail(TDOA_ERR_NOMEM, "hipMalloc of context tables failed");
+    }
+    hipError_t e = hipMemcpy(c->d_window, w16.data(), sizeof(int16_t) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_prior, c->prior.data(), sizeof(float) * c->K, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_tuples, c->tuples.data(), sizeof(uint32_t) * c->tuples.size(),
+                      hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_tuple_cell, c->tuple_cell.data(), sizeof(int32_t) * c->U,
+                      hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        free_device(c);
+        delete c;
+        return fail(TDOA_ERR_HIP, "uploading context tables: %s", hipGetErrorString(e));
+    }
+    kp.window = c->d_window;
+    kp.prior = c->d_prior;
+    kp.tuples = c->d_tuples;
+    kp.tuple_cell = c->d_tuple_cell;
+    *out = c;
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_destroy(tdoa_ctx *ctx)
+{
+    if (!ctx)
+        return TDOA_OK;
+    (void)hipSetDevice(ctx->device);
+    free_device(ctx);
+    delete ctx;
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_get_dims(const tdoa_ctx *c, int32_t *M, int32_t *N, int32_t *P,
+                             int32_t *K, int32_t *G)
+{
+    if (!c)
+        return fail(TDOA_ERR_INVALID, "tdoa_get_dims: NULL ctx");
+    if (M)
+        *M = c->M;
+    if (N)
+        *N = c->N;
+    if (P)
+        *P = c->P;
+    if (K)
+        *K = c->K;
+    if (G)
+        *G = c->G;
+    return TDOA_OK;
+}
+
+static tdoa_kout to_kout(const tdoa_outputs *o)
+{
+    tdoa_kout k;
+    k.lags = o->lags;
+    k.gate = o->gate;
+    k.cell = o->cell;
+    k.xy = o->xy;
+    k.max_L = o->max_L;
+    k.max_Lf = o->max_Lf;
+    k.scores = o->scores;
+    k.weighted = o->weighted;
+    k.scores_f = o->scores_f;
+    k.weighted_f = o->weighted_f;
+    return k;
+}
+
+static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,
+                     void *stream, bool prepared)
+{
+    if (!ctx || !out || (!frames && B > 0))
+        return fail(TDOA_ERR_INVALID, "localize: NULL argument");
+    if (B < 0)
+        return fail(TDOA_ERR_INVALID, "localize: negative batch");
+    if (!out->lags)
+        return fail(TDOA_ERR_INVALID, "localize: outputs.lags is required");
+    if (B == 0)
+        return TDOA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT && !prepared)
+        return tdoa_launch_gcc_phat(ctx->kp, to_kout(out), frames, B, ctx->cfg.phat_eps, stream);
+    return tdoa_launch_direct(ctx->kp, to_kout(out), frames, B, prepared, stream, nullptr);
+}
+
+extern "C" int tdoa_localize_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B,
+                                   const tdoa_outputs *out, void *stream)
+{
+    return run_batch(ctx, frames, B, out, stream, false);
+}
+
+extern "C" int tdoa_correlate_prepared(tdoa_ctx *ctx, const int16_t *prepared, int64_t B,
+                                       const tdoa_outputs *out, void *stream)
+{
+    return run_batch(ctx, prepared, B, out, stream, true);
+}
+
+extern "C" int tdoa_average_batch(tdoa_ctx *ctx, int64_t S, int64_t *est, const int64_t *fresh,
+                                  const float *decay, int32_t *best, const tdoa_outputs *solve,
+                                  void *stream)
+{
+    if (!ctx || !est || !fresh || !decay || !best)
+        return fail(TDOA_ERR_INVALID, "tdoa_average_batch: NULL argument");
+    if (S < 0)
+        return fail(TDOA_ERR_INVALID, "tdoa_average_batch: negative stream count");
+    if (S == 0)
+        return TDOA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    tdoa_kout k;
+    const tdoa_kout *kptr = nullptr;
+    if (solve) {
+        k = to_kout(solve);
+        kptr = &k;
+    }
+    return tdoa_launch_average(ctx->kp, S, est, fresh, decay, best, kptr, stream);
+}
+
+// correlations.c:40-43
+extern "C" float tdoa_decay_us(uint64_t now_us, uint64_t last_us)
+{
+    const float dt = (float)(now_us - last_us) / 1e6f;
+    const float arg = -dt / 0.5f;
+    return (float)(1.0 - std::exp((double)arg));
+}
+
+extern "C" int tdoa_get_window(const tdoa_ctx *c, int32_t *w)
+{
+    if (!c || !w)
+        return fail(TDOA_ERR_INVALID, "NULL");
+    std::memcpy(w, c->win.data(), sizeof(int32_t) * c->N);
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_get_mics(const tdoa_ctx *c, float *xy)
+{
+    if (!c || !xy)
+        return fail(TDOA_ERR_INVALID, "NULL");
+    std::memcpy(xy, c->mic.data(), sizeof(float) * 2 * c->M);
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_get_lut(const tdoa_ctx *c, uint8_t *lut)
+{
+    if (!c || !lut)
+        return fail(TDOA_ERR_INVALID, "NULL");
+    std::memcpy(lut, c->lut.data(), c->lut.size());
+    return TDOA_OK;
+}
+
+extern "C" int tdoa_get_prior(const tdoa_ctx *c, float *scale)
+{
+    if (!c || !scale)
+        return fail(TDOA_ERR_INVALID, "NULL");
+    std::memcpy(scale, c->prior.data(), sizeof(float) * c->K);
+    return TDOA_OK;
+}
+
+extern "C" const char *tdoa_last_error(void) { return g_err.c_str(); }
+
+extern "C" int tdoa_abi_version(void) { return TDOA_ABI_VERSION; }
+
+// used by tdoa_kernels.hip launchers
+int tdoa_set_error(int code, const char *msg)
+{
+    g_err = msg;
+    return code;
+}

@@ -1,0 +1,63 @@
+// tdoa_internal.h -- layout contract between the host side (tdoa_capi.cpp)
+// and the gfx950 kernels (tdoa_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <stdint.h>
+
+#define TDOA_MAX_PAIRS 28  // 8 mics
+
+// Lag tiling of the DIRECT kernel: each work item owns TDOA_LT consecutive
+// lags (an even start lag, so even lags read word-aligned sample pairs and odd
+// lags read the one-sample-shifted pairs) over a TDOA_SEGW-word (2*SEGW
+// sample) segment of the frame.  SEGW <= 128 keeps every int32 partial of the
+// hi/lo byte-split products exact (256 * 32768 * 255 < 2^31).
+#define TDOA_LT 16
+#define TDOA_LT2 (TDOA_LT / 2)
+#define TDOA_SEGW 64
+
+struct tdoa_kparams {
+    // shape
+    int32_t M, N, log2N, P, K, S;  // S = max_shift, K = 2S+1
+    int32_t G, U;                  // grid cells, unique lag tuples
+    int32_t grid_W, half_w, half_h;
+    float grid_scale;
+    // DIRECT tiling
+    int32_t sbase;   // first (even) lag of tile 0
+    int32_t T;       // lag tiles per pair
+    int32_t NSEG;    // segments per frame row (N/2 / SEGW)
+    int32_t PADW;    // zero words left/right of every staged row
+    int32_t RS;      // staged row stride in words = N/2 + 2*PADW
+    int32_t F;       // frames per workgroup
+    int32_t TW;      // tuple words per lag tuple = ceil(P/4)
+    uint8_t pair_i[TDOA_MAX_PAIRS];
+    uint8_t pair_j[TDOA_MAX_PAIRS];
+    // device tables
+    const int16_t *window;     // [N] Q15
+    const float *prior;        // [K] scale by |s - best|
+    const uint32_t *tuples;    // [U][TW] packed lag indices (byte p = pair p)
+    const int32_t *tuple_cell; // [U] first row-major cell of each tuple
+};
+
+struct tdoa_kout {
+    int32_t *lags;
+    uint8_t *gate;
+    int32_t *cell;
+    float *xy;
+    int64_t *max_L;
+    float *max_Lf;
+    int64_t *scores;
+    int64_t *weighted;
+    float *scores_f;
+    float *weighted_f;
+};
+
+// Host-side launchers implemented in tdoa_kernels.hip.
+int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
+                       const int16_t *frames, int64_t B, bool prepared,
+                       void *stream, int *lds_bytes_out);
+int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est,
+                        const int64_t *fresh, const float *decay, int32_t *best,
+                        const tdoa_kout *solve, void *stream);
+int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
+                         const int16_t *frames, int64_t B, float phat_eps,
+                         void *stream);

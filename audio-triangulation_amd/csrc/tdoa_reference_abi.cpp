@@ -1,0 +1,256 @@
+// tdoa_reference_abi.cpp -- the reference's per-frame component symbols
+// (include/tdoa_reference_abi.h) on top of libtdoa.
+//
+// GPU-backed (one-frame launches, synchronous, abort on HIP failure):
+//   rolling_buffer_write_out  rolling_buffer.c:43-71
+//   buffer_normalize_range    buffer.c:13-18
+//   buffer_window             buffer.c:4-11
+//   correlations_init         correlations.c:4-36   (via tdoa_correlate_prepared)
+//   correlations_average      correlations.c:38-63  (via tdoa_average_batch)
+// Host (capture ring / one-time geometry):
+//   rolling_buffer_init/push/get_*_power  rolling_buffer.c:3-41,73-85
+//   microphones_init                      microphones.c:9-33
+
+#include "../../include/tdoa_reference_abi.h"
+#include "../../include/tdoa.h"
+#include "tdoa_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <time.h>
+
+int tdoa_launch_ref_buffer(int op, int16_t *buf, const int16_t *ring, int head, int64_t *power,
+                           const int16_t *window, int n, void *stream);
+
+point2d_t mic_a_location;
+point2d_t mic_b_location;
+point2d_t mic_c_location;
+
+static_assert(sizeof(struct buffer_t) == 2056, "buffer_t layout (x86-64)");
+static_assert(sizeof(struct correlations_t) == 760, "correlations_t layout (x86-64)");
+static_assert(sizeof(struct rolling_buffer_t) == 2088 || sizeof(struct rolling_buffer_t) == 2096,
+              "rolling_buffer_t layout");
+
+namespace {
+
+absolute_time_t default_clock()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (absolute_time_t)ts.tv_sec * 1000000u + (absolute_time_t)(ts.tv_nsec / 1000);
+}
+
+absolute_time_t (*g_clock)(void) = default_clock;
+int g_device = 0;
+
+// One lazily created 2-mic context (pair = (buf_a, buf_b)) plus device
+// staging buffers; the reference's functions are single-threaded, guard anyway.
+struct RefState {
+    std::mutex mu;
+    bool ready = false;
+    tdoa_ctx *ctx = nullptr;
+    int16_t *d_frames = nullptr;   // [2][1024]
+    int16_t *d_ring = nullptr;     // [1024]
+    int64_t *d_i64 = nullptr;      // scores/weighted/est/fresh scratch
+    int32_t *d_i32 = nullptr;
+    float *d_f32 = nullptr;
+    int16_t *d_window = nullptr;   // Q15 DPSS(1024, 2)
+} g_ref;
+
+[[noreturn]] void die(const char *what)
+{
+    std::fprintf(stderr, "libtdoa reference shim: %s: %s\n", what, tdoa_last_error());
+    std::abort();
+}
+
+void check(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "libtdoa reference shim: %s: %s\n", what, hipGetErrorString(e));
+        std::abort();
+    }
+}
+
+RefState &ref()
+{
+    if (g_ref.ready)
+        return g_ref;
+    std::lock_guard<std::mutex> lk(g_ref.mu);
+    if (g_ref.ready)
+        return g_ref;
+    tdoa_config cfg;
+    tdoa_config_default(&cfg);
+    cfg.num_mics = 2;
+    const float two_mics[4] = {-0.066f, 0.0f, 0.066f, 0.0f};  // grid unused here
+    cfg.mic_xy = two_mics;
+    cfg.grid_half_w = 0;
+    cfg.grid_half_h = 0;
+    if (tdoa_create(&cfg, g_device, &g_ref.ctx) != TDOA_OK)
+        die("tdoa_create");
+    check(hipMalloc(&g_ref.d_frames, 2 * 1024 * sizeof(int16_t)), "hipMalloc");
+    check(hipMalloc(&g_ref.d_ring, 1024 * sizeof(int16_t)), "hipMalloc");
+    check(hipMalloc(&g_ref.d_i64, 4 * 128 * sizeof(int64_t)), "hipMalloc");
+    check(hipMalloc(&g_ref.d_i32, 64 * sizeof(int32_t)), "hipMalloc");
+    check(hipMalloc(&g_ref.d_f32, 64 * sizeof(float)), "hipMalloc");
+    check(hipMalloc(&g_ref.d_window, 1024 * sizeof(int16_t)), "hipMalloc");
+    int32_t w[1024];
+    tdoa_get_window(g_ref.ctx, w);
+    int16_t w16[1024];
+    for (int i = 0; i < 1024; i++)
+        w16[i] = (int16_t)w[i];
+    check(hipMemcpy(g_ref.d_window, w16, sizeof w16, hipMemcpyHostToDevice), "hipMemcpy");
+    g_ref.ready = true;
+    return g_ref;
+}
+
+// One op of k_ref_buffer on a single 1024-sample buffer.
+void buffer_op(int op, struct buffer_t *dst, const struct rolling_buffer_t *ring)
+{
+    RefState &R = ref();
+    check(hipSetDevice(g_device), "hipSetDevice");
+    int16_t *d_buf = R.d_frames;
+    if (ring)
+        check(hipMemcpy(R.d_ring, ring->buffer, sizeof ring->buffer, hipMemcpyHostToDevice),
+              "hipMemcpy");
+    else
+        check(hipMemcpy(d_buf, dst->buffer, sizeof dst->buffer, hipMemcpyHostToDevice),
+              "hipMemcpy");
+    if (tdoa_launch_ref_buffer(op, d_buf, R.d_ring, ring ? ring->head : 0, R.d_i64, R.d_window,
+                               TDOA_REF_BUFFER_SIZE, nullptr) != 0)
+        die("k_ref_buffer");
+    check(hipMemcpy(dst->buffer, d_buf, sizeof dst->buffer, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (op == 0)
+        check(hipMemcpy(&dst->power, R.d_i64, sizeof(int64_t), hipMemcpyDeviceToHost),
+              "hipMemcpy");
+}
+
+}  // namespace
+
+extern "C" void tdoa_ref_set_clock(absolute_time_t (*now_us)(void))
+{
+    g_clock = now_us ? now_us : default_clock;
+}
+
+extern "C" int tdoa_ref_set_device(int device)
+{
+    if (g_ref.ready)
+        return TDOA_ERR_INVALID;
+    g_device = device;
+    return TDOA_OK;
+}
+
+// ------------------------------------------------------------ microphones
+// microphones.c:9-33 (MIRROR_MICROPHONES true, ROTATE_MICROPHONES false)
+extern "C" void microphones_init(void)
+{
+    const float dAB = 0.132f, dBC = 0.15f, dCA = 0.20f;
+    const float xC = (dAB * dAB + dCA * dCA - dBC * dBC) / (2.0f * dAB);
+    const float yC = sqrtf(fmaxf(0.0f, dCA * dCA - xC * xC));
+    const point2d_t pA = {0.0f, 0.0f}, pB = {dAB, 0.0f}, pC = {xC, yC * -1.0f};
+    const float cx = (pA.x + pB.x + pC.x) / 3.0f;
+    const float cy = (pA.y + pB.y + pC.y) / 3.0f;
+    mic_a_location = {pA.x - cx, pA.y - cy};
+    mic_b_location = {pB.x - cx, pB.y - cy};
+    mic_c_location = {pC.x - cx, pC.y - cy};
+}
+
+// ------------------------------------------------------ capture ring (host)
+extern "C" void rolling_buffer_init(struct rolling_buffer_t *b)
+{
+    b->head = 0;
+    b->incoming_power = b->incoming_total = 0;
+    b->outgoing_power = b->outgoing_total = 0;
+    b->is_full = false;
+    std::memset(b->buffer, 0, sizeof b->buffer);
+}
+
+// rolling_buffer.c:16-41: the sample at head-N/2 crosses from the newer half
+// to the older half; the sample at head leaves the older half.
+extern "C" void rolling_buffer_push(struct rolling_buffer_t *b, sample_t sample)
+{
+    const int n = TDOA_REF_BUFFER_SIZE;
+    int mid = b->head - n / 2;
+    if (mid < 0)
+        mid += n;
+    const int64_t m = b->buffer[mid], o = b->buffer[b->head], s = sample;
+    b->outgoing_total += m - o;
+    b->outgoing_power += m * m - o * o;
+    b->incoming_total += s - m;
+    b->incoming_power += s * s - m * m;
+    b->buffer[b->head] = sample;
+    if (++b->head >= n) {
+        b->head = 0;
+        b->is_full = true;
+    }
+}
+
+// rolling_buffer.c:73-85 with BUFFER_HALF_SIZE_BITS = 9
+extern "C" power_t rolling_buffer_get_incoming_power(const struct rolling_buffer_t *b)
+{
+    return (power_t)((uint64_t)b->incoming_power << 9) - b->incoming_total * b->incoming_total;
+}
+
+extern "C" power_t rolling_buffer_get_outgoing_power(const struct rolling_buffer_t *b)
+{
+    return (power_t)((uint64_t)b->outgoing_power << 9) - b->outgoing_total * b->outgoing_total;
+}
+
+// ------------------------------------------------------------- GPU-backed
+extern "C" void rolling_buffer_write_out(const struct rolling_buffer_t *b, struct buffer_t *dst)
+{
+    buffer_op(0, dst, b);
+}
+
+extern "C" void buffer_normalize_range(struct buffer_t *buf) { buffer_op(1, buf, nullptr); }
+
+extern "C" void buffer_window(struct buffer_t *buf) { buffer_op(2, buf, nullptr); }
+
+extern "C" void correlations_init(struct correlations_t *corr, const struct buffer_t *a,
+                                  const struct buffer_t *b)
+{
+    RefState &R = ref();
+    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipMemcpy(R.d_frames, a->buffer, sizeof a->buffer, hipMemcpyHostToDevice), "hipMemcpy");
+    check(hipMemcpy(R.d_frames + TDOA_REF_BUFFER_SIZE, b->buffer, sizeof b->buffer,
+                    hipMemcpyHostToDevice),
+          "hipMemcpy");
+    tdoa_outputs o;
+    std::memset(&o, 0, sizeof o);
+    o.lags = R.d_i32;
+    o.weighted = R.d_i64;
+    if (tdoa_correlate_prepared(R.ctx, R.d_frames, 1, &o, nullptr) != TDOA_OK)
+        die("correlations_init");
+    check(hipMemcpy(corr->correlations, R.d_i64, sizeof corr->correlations, hipMemcpyDeviceToHost),
+          "hipMemcpy");
+    int32_t best = 0;
+    check(hipMemcpy(&best, R.d_i32, sizeof best, hipMemcpyDeviceToHost), "hipMemcpy");
+    corr->best_shift = best;
+    corr->last_update = g_clock();
+}
+
+extern "C" void correlations_average(struct correlations_t *est, struct correlations_t *fresh)
+{
+    RefState &R = ref();
+    check(hipSetDevice(g_device), "hipSetDevice");
+    const absolute_time_t now = g_clock();
+    const float decay = tdoa_decay_us(now, est->last_update);
+    int64_t *d_est = R.d_i64, *d_new = R.d_i64 + 128;
+    check(hipMemcpy(d_est, est->correlations, sizeof est->correlations, hipMemcpyHostToDevice),
+          "hipMemcpy");
+    check(hipMemcpy(d_new, fresh->correlations, sizeof fresh->correlations, hipMemcpyHostToDevice),
+          "hipMemcpy");
+    check(hipMemcpy(R.d_f32, &decay, sizeof decay, hipMemcpyHostToDevice), "hipMemcpy");
+    if (tdoa_average_batch(R.ctx, 1, d_est, d_new, R.d_f32, R.d_i32, nullptr, nullptr) != TDOA_OK)
+        die("correlations_average");
+    check(hipMemcpy(est->correlations, d_est, sizeof est->correlations, hipMemcpyDeviceToHost),
+          "hipMemcpy");
+    int32_t best = 0;
+    check(hipMemcpy(&best, R.d_i32, sizeof best, hipMemcpyDeviceToHost), "hipMemcpy");
+    est->best_shift = best;
+    est->last_update = now;
+}

@@ -1,0 +1,150 @@
+/*
+ * tdoa.h -- batched C ABI of the MI355X TDOA localizer (libtdoa.so).
+ *
+ * The reference (yuan-xy/Audio-Triangulation) processes one 3-mic frame at a
+ * time inside protothread_sample_and_compute (src/sample_compute.h:105-139)
+ * and solves the position on a 101x101 grid in vga_draw_heatmap
+ * (src/components/vga/vga_heatmap.h:95-108).  This header is the batched,
+ * error-returning form of that path: one call runs, for B frames at once,
+ *
+ *   rolling_buffer_write_out DC removal  rolling_buffer.c:64-66
+ *   buffer_normalize_range (<<8 wrap)     buffer.c:13-18
+ *   buffer_window (Q15 DPSS NW=2)         buffer.c:4-11, window.ipynb:43-60
+ *   correlations_init (scores, argmax,    correlations.c:4-36
+ *                      Gaussian lag prior)
+ *   shift gate sum(best^2) > 4            sample_compute.h:124-134
+ *   grid L = sum_p corr_p[LUT_p] max pass vga_heatmap.h:48-108
+ *
+ * as hand-written gfx950 kernels.  The per-frame reference symbols live in
+ * tdoa_reference_abi.h and are implemented on top of this API.
+ *
+ * Conventions: all pointers in tdoa_outputs and the frames pointer of
+ * tdoa_localize_batch are DEVICE pointers on the context's device; `stream`
+ * is a hipStream_t (NULL = default stream).  Every function returns
+ * TDOA_OK (0) or a negative tdoa_status; tdoa_last_error() describes the
+ * last failure on the calling thread.  A context is bound to one device and
+ * is not thread-safe: use one context per host thread / GPU.
+ */
+#ifndef TDOA_H
+#define TDOA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TDOA_ABI_VERSION 1
+#define TDOA_MAX_MICS 8
+
+typedef enum tdoa_status {
+    TDOA_OK = 0,
+    TDOA_ERR_INVALID = -1,   /* bad argument / config */
+    TDOA_ERR_HIP = -2,       /* HIP runtime error (message in tdoa_last_error) */
+    TDOA_ERR_NO_DEVICE = -3, /* no gfx950 device visible */
+    TDOA_ERR_NOMEM = -4
+} tdoa_status;
+
+typedef enum tdoa_engine {
+    /* Exact integer time-domain cross-correlation: the reference's
+     * correlations_init semantics bit-for-bit (int64 scores). */
+    TDOA_ENGINE_DIRECT = 0,
+    /* Generalised cross-correlation with PHAT weighting (fp32 radix-4 FFT,
+     * |X| normalised cross-spectrum, inverse FFT), the north-star
+     * formulation.  Float scores; lags equal DIRECT's on clean integer
+     * delays, otherwise checked against a float64 GCC-PHAT oracle. */
+    TDOA_ENGINE_GCC_PHAT = 1
+} tdoa_engine;
+
+typedef struct tdoa_config {
+    int32_t num_mics;        /* M, 2..TDOA_MAX_MICS              (reference: 3) */
+    int32_t frame_len;       /* N, power of two 256..4096        (buffer.h:5-6: 1024) */
+    int32_t sample_rate_hz;  /* fs                               (constants.h:10: 50000) */
+    int32_t max_shift;       /* <= 0 -> fs*32/34300              (constants.h:12: 46) */
+    float speed_of_sound;    /* m/s                              (constants.h:14: 343) */
+    int32_t engine;          /* tdoa_engine */
+    /* mic positions [M][2] in metres; NULL -> microphones_init()'s triangle
+     * (microphones.c:9-33) for M == 3, otherwise required. Copied. */
+    const float *mic_xy;
+    /* grid (vga.h:29-35, vga_heatmap.h:2-3): (2*half_w+1) x (2*half_h+1)
+     * cells at grid_scale cells per metre, projected on a hemisphere of
+     * radius height_offset. */
+    int32_t grid_half_w;     /* 50 */
+    int32_t grid_half_h;     /* 50 */
+    float grid_scale;        /* 24.0f */
+    float height_offset;     /* 1.2f */
+    /* Q15 window [N]; NULL -> DPSS(N, NW=2) normalised to max 1, x32767,
+     * rounded (window.ipynb procedure; equals window_function.h at N=1024).
+     * Copied. */
+    const int32_t *window_q15;
+    float phat_eps;          /* GCC_PHAT: |cross| floor, default 1e-20f */
+} tdoa_config;
+
+/* Per-frame results (device pointers; any may be NULL unless noted). */
+typedef struct tdoa_outputs {
+    int32_t *lags;           /* [B][P] best shift per pair (required)       */
+    uint8_t *gate;           /* [B] sum_p lag^2 > 4 (sample_compute.h:134)   */
+    int32_t *cell;           /* [B] first row-major argmax cell of L         */
+    float *xy;               /* [B][2] ((x-hw)/scale, (hh-y)/scale) metres   */
+    int64_t *max_L;          /* [B] DIRECT: max of L (vga_heatmap.h:99-108)  */
+    float *max_Lf;           /* [B] GCC_PHAT: max of L                       */
+    int64_t *scores;         /* [B][P][K] DIRECT raw int64 scores (debug)    */
+    int64_t *weighted;       /* [B][P][K] DIRECT scores after the lag prior  */
+    float *scores_f;         /* [B][P][K] GCC_PHAT raw correlation (debug)   */
+    float *weighted_f;       /* [B][P][K] GCC_PHAT after the lag prior       */
+} tdoa_outputs;
+
+typedef struct tdoa_ctx tdoa_ctx;
+
+/* Fills the reference defaults (3 mics, 1024, 50 kHz, 46, DIRECT, ...). */
+int tdoa_config_default(tdoa_config *cfg);
+
+/* Validates cfg, builds the window, mic geometry, lag prior table and the
+ * grid LUT on the host, uploads them to `device`. */
+int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out);
+int tdoa_destroy(tdoa_ctx *ctx);
+
+/* Derived sizes of a context. */
+int tdoa_get_dims(const tdoa_ctx *ctx, int32_t *M, int32_t *N, int32_t *P,
+                  int32_t *K, int32_t *G);
+
+/* Stateless batch: frames = device int16 [B][M][N] raw (pre-DC) samples, mic
+ * rows contiguous.  Asynchronous on `stream`. */
+int tdoa_localize_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B,
+                        const tdoa_outputs *out, void *stream);
+
+/* Same as tdoa_localize_batch for frames that already went through DC
+ * removal, normalisation and the window (the inputs correlations_init sees).
+ * Used by the per-frame reference symbols. */
+int tdoa_correlate_prepared(tdoa_ctx *ctx, const int16_t *prepared, int64_t B,
+                            const tdoa_outputs *out, void *stream);
+
+/* Temporal averaging (correlations.c:38-63) for S independent streams:
+ * est[S][P][K] (device, in/out) <- (int64)((float)est + (float)(fresh-est)*decay[s]),
+ * best[S][P] re-argmaxed.  decay (device float[S]) comes from
+ * tdoa_decay_us on the host.  If solve is non-NULL the grid solve runs on the
+ * averaged scores (the reference solves on corr_*, vga_heatmap.h:102-104). */
+int tdoa_average_batch(tdoa_ctx *ctx, int64_t S, int64_t *est,
+                       const int64_t *fresh, const float *decay, int32_t *best,
+                       const tdoa_outputs *solve, void *stream);
+
+/* Host helper: decay of correlations.c:42-43 from integer-us timestamps. */
+float tdoa_decay_us(uint64_t now_us, uint64_t last_us);
+
+/* Host copies of the context's tables (for tests / tooling). */
+int tdoa_get_window(const tdoa_ctx *ctx, int32_t *window /* [N] */);
+int tdoa_get_mics(const tdoa_ctx *ctx, float *mic_xy /* [M][2] */);
+int tdoa_get_lut(const tdoa_ctx *ctx, uint8_t *lut /* [P][G] */);
+int tdoa_get_prior(const tdoa_ctx *ctx, float *scale /* [K] by |d| */);
+
+/* DPSS(N, NW) first Slepian taper, Q15 as in window.ipynb. */
+int tdoa_dpss_q15(int32_t n, double nw, int32_t *out);
+
+const char *tdoa_last_error(void);
+int tdoa_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDOA_H */

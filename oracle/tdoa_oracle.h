@@ -1,0 +1,107 @@
+/*
+ * tdoa_oracle.h -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE).
+ *
+ * THIS IS THE CHECKER, NOT THE PRODUCT.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product path
+ * (audio-triangulation_amd/, libtdoa.so) never links or calls it.
+ *
+ * Restates yuan-xy/Audio-Triangulation's integer/float semantics, generalised
+ * to M mics, N samples (power of two), P = M(M-1)/2 pairs, K = 2*max_shift+1:
+ *   rolling_buffer.c:3-85   ring, half powers, linearise + floor-mean DC removal
+ *   buffer.c:4-18           <<8 (int16 wrap) and Q15 window
+ *   correlations.c:4-63     int64 xcorr, first-max argmax, Gaussian prior, EMA
+ *   microphones.c:9-33      3-mic law-of-cosines geometry
+ *   vga_heatmap.h:48-108    per-cell lag LUT and L = sum_p corr_p[LUT_p] max pass
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - rolling buffer, normalize, window, microphones: pinned bit-exact against
+ *     the reference's own buffer.c / rolling_buffer.c / microphones.c compiled
+ *     unchanged into oracle/_ref (oracle/Makefile) -- tests/test_oracle_pin.py.
+ *   - window tables: pinned against window_function.h:5-70 (N=1024) and the
+ *     notebook's stored output window.ipynb:73-202 (N=2048).
+ *   - correlations.c / vga_heatmap.h: the reference TUs need Pico SDK headers
+ *     (pico/time.h, lib/vga/...) that this image lacks, so they are
+ *     UNBUILDABLE here: those stages are "parity unpinned" by reference output
+ *     and are checked by an independent numpy restatement plus known-answer
+ *     (injected integer delay) cases.
+ *
+ * Compile with -ffp-contract=off and without -ffast-math: FMA contraction
+ * changes correlations_average.
+ */
+#ifndef TDOA_ORACLE_H
+#define TDOA_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- a3: linearised-frame DC removal (rolling_buffer.c:43-71) ---- */
+void orc_dc_remove(const int16_t *in, int16_t *out, int n, int64_t *power);
+
+/* ---- rolling ring restatement (rolling_buffer.c:3-85) ---- */
+typedef struct orc_ring {
+    int head;
+    int64_t incoming_power, incoming_total;
+    int64_t outgoing_power, outgoing_total;
+    int is_full;
+    int n;
+    int16_t *buf; /* n samples, caller-owned */
+} orc_ring;
+void orc_ring_init(orc_ring *r, int16_t *storage, int n);
+void orc_ring_push(orc_ring *r, int16_t sample);
+void orc_ring_write_out(const orc_ring *r, int16_t *dst, int64_t *power);
+int64_t orc_ring_incoming_power(const orc_ring *r);
+int64_t orc_ring_outgoing_power(const orc_ring *r);
+
+/* ---- a4/a5: buffer.c:13-18 and buffer.c:4-11 ---- */
+void orc_normalize(int16_t *x, int n);
+void orc_window(int16_t *x, const int32_t *w, int n);
+
+/* ---- a6/a7: correlations.c:4-36 ---- */
+void orc_xcorr(const int16_t *a, const int16_t *b, int n, int max_shift,
+               int64_t *scores, int32_t *best);
+float orc_prior_scale(int d2); /* (float)exp(-d2/36.f)   correlations.c:30 */
+void orc_prior(int64_t *scores, int max_shift, int best);
+
+/* ---- a9: correlations.c:38-63 ---- */
+float orc_decay(uint64_t now_us, uint64_t last_us);
+void orc_average(int64_t *est, const int64_t *fresh, int K, float decay,
+                 int32_t *best);
+
+/* ---- a10: microphones.c:9-33 (reference triangle, MIRROR on, ROTATE off) ---- */
+void orc_microphones_ref(float xy[6]);
+
+/* ---- a11: vga_heatmap.h:48-93 generalised to M mics, lexicographic pairs ---- */
+void orc_build_lut(const float *mic_xy, int M, int half_w, int half_h,
+                   float grid_scale, float height, float speed_of_sound,
+                   int fs, int max_shift, uint8_t *lut /* [P][H][W] */);
+
+/* ---- a12: vga_heatmap.h:99-108 max pass + argmax extension ---- */
+void orc_grid_solve(const int64_t *weighted /* [P][K] */, int P, int K,
+                    const uint8_t *lut /* [P][G] */, int G,
+                    int64_t *max_L, int32_t *cell);
+
+/* ---- full stateless pipeline over a batch (sample_compute.h:105-134 +
+ *      vga_heatmap.h:99-108), OpenMP over frames ---- */
+typedef struct orc_batch_out {
+    int64_t *scores;   /* [B][P][K] raw, may be NULL */
+    int64_t *weighted; /* [B][P][K] after prior, may be NULL */
+    int32_t *lags;     /* [B][P] */
+    uint8_t *gate;     /* [B] */
+    int32_t *cell;     /* [B] */
+    int64_t *max_L;    /* [B] */
+    float *xy;         /* [B][2] */
+} orc_batch_out;
+
+int orc_localize_batch(const int16_t *frames /* [B][M][N] raw */, int64_t B,
+                       int M, int N, int max_shift, const int32_t *window,
+                       const uint8_t *lut, int half_w, int half_h,
+                       float grid_scale, int do_grid, int threads,
+                       orc_batch_out *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,217 @@
+"""Parity of libtdoa's gfx950 kernels (through the C ABI) with the oracle.
+
+DIRECT engine: bit-exact for every integer output (scores, weighted scores,
+lags, gate, grid max, argmax cell) and exact float32 (x, y).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+import tdoa  # noqa: E402
+from tdoa import _lib, synth  # noqa: E402
+from tdoa.localizer import Localizer  # noqa: E402
+
+
+def _np(d):
+    return {k: v.cpu().numpy() for k, v in d.items()}
+
+
+def _cmp(got, exp, keys=("lags", "gate", "cell", "max_L", "xy", "scores", "weighted")):
+    for k in keys:
+        if k in exp and k in got:
+            g, e = got[k], exp[k]
+            bad = np.argwhere(g != e) if g.shape == e.shape else None
+            assert g.shape == e.shape and bad.size == 0, \
+                f"{k}: {0 if bad is None else len(bad)} mismatches, first {None if bad is None else bad[:3].tolist()}"
+
+
+@pytest.fixture(scope="module")
+def loc3():
+    return Localizer()
+
+
+def test_golden_pipeline_cfg2(loc3):
+    g = golden("pipeline_cfg2.npz")
+    assert (loc3.lut().reshape(g["lut"].shape) == g["lut"]).all()
+    fr = torch.from_numpy(g["frames"]).cuda()
+    got = _np(loc3.localize(fr, scores=True))
+    _cmp(got, dict(g))
+
+
+def test_cfg2_batch_vs_oracle(loc3, oracle):
+    lut = loc3.lut().reshape(3, 101, 101)
+    fr, cells, tau = synth.adc_frames(4096, 3, 1024, lut, 46, synth.SEEDS[2], device="cuda")
+    got = _np(loc3.localize(fr, scores=True))
+    exp = oracle.localize_batch(fr.cpu().numpy(), 46, loc3.window(), lut, threads=8)
+    _cmp(got, exp)
+    # known answer: pair (0, m) lags recover the injected integer delays
+    agree = (got["lags"][:, :2] == tau.cpu().numpy()[:, 1:]).mean()
+    assert agree > 0.95
+
+
+def test_full_range_int16_wrap(loc3, oracle):
+    fr = synth.full_range_frames(512, 3, 1024, 0xABC, device="cuda")
+    got = _np(loc3.localize(fr, scores=True))
+    exp = oracle.localize_batch(fr.cpu().numpy(), 46, loc3.window(), loc3.lut().reshape(3, 101, 101),
+                                threads=8)
+    _cmp(got, exp)
+
+
+@pytest.mark.parametrize("B", [1, 2, 3, 5, 7, 9, 33])
+def test_ragged_batches(loc3, oracle, B):
+    lut = loc3.lut().reshape(3, 101, 101)
+    fr, _, _ = synth.adc_frames(B, 3, 1024, lut, 46, 1000 + B, device="cuda")
+    got = _np(loc3.localize(fr, scores=True))
+    exp = oracle.localize_batch(fr.cpu().numpy(), 46, loc3.window(), lut)
+    _cmp(got, exp)
+
+
+def test_empty_batch(loc3):
+    fr = torch.empty((0, 3, 1024), dtype=torch.int16, device="cuda")
+    out = loc3.localize(fr)
+    assert out["lags"].shape == (0, 3)
+
+
+def test_constant_frames_tie_break(loc3, oracle):
+    # all-equal frames: every score 0 -> first lag (-S) wins, as in correlations.c:20
+    fr = torch.full((4, 3, 1024), 128, dtype=torch.int16, device="cuda")
+    got = _np(loc3.localize(fr, scores=True))
+    exp = oracle.localize_batch(fr.cpu().numpy(), 46, loc3.window(), loc3.lut().reshape(3, 101, 101))
+    _cmp(got, exp)
+    assert (got["lags"] == -46).all()
+
+
+CONFIGS = [
+    # (M, N, fs, max_shift, mics, half)
+    (2, 1024, 50000, 0, np.array([[-0.066, 0.0], [0.066, 0.0]], np.float32), 50),
+    (3, 1024, 48000, 0, None, 50),            # 48 kHz -> S = 44
+    (3, 1024, 50000, 45, None, 50),           # odd S: lag tiles start at -S-1
+    (3, 256, 50000, 0, None, 20),
+    (3, 512, 50000, 0, None, 50),
+    (4, 4096, 50000, 0, synth.square_mics(0.15), 50),
+    (8, 2048, 50000, 0, synth.circle_mics(8, 0.15), 50),
+    (5, 2048, 50000, 63, synth.circle_mics(5, 0.3), 30),
+]
+
+
+@pytest.mark.parametrize("M,N,fs,S_cfg,mics,half", CONFIGS)
+def test_configs_vs_oracle(oracle, M, N, fs, S_cfg, mics, half):
+    loc = Localizer(num_mics=M, frame_len=N, sample_rate_hz=fs, max_shift=S_cfg, mic_xy=mics,
+                    grid_half_w=half, grid_half_h=half)
+    S = loc.dims.S
+    lut = loc.lut()
+    mic_xy = loc.mics()
+    exp_lut = oracle.build_lut(mic_xy, half_w=half, half_h=half, fs=fs, max_shift=S)
+    assert (lut == exp_lut.reshape(lut.shape)).all()
+    assert (loc.window() == tdoa.dpss_q15(N)).all()
+    B = 48 if N <= 2048 else 24
+    fr, _, _ = synth.adc_frames(B, M, N, exp_lut, S, 77 + M + N, device="cuda")
+    fr2 = synth.full_range_frames(8, M, N, 99 + N, device="cuda")
+    fr = torch.cat([fr, fr2]).contiguous()
+    got = _np(loc.localize(fr, scores=True))
+    exp = oracle.localize_batch(fr.cpu().numpy(), S, loc.window(), exp_lut,
+                                half_w=half, half_h=half, threads=8)
+    _cmp(got, exp)
+
+
+def test_prepared_path_arbitrary_int16(oracle):
+    loc = Localizer(num_mics=2, mic_xy=np.array([[-0.066, 0], [0.066, 0]], np.float32))
+    g = torch.Generator().manual_seed(5)
+    fr = torch.randint(-32768, 32768, (64, 2, 1024), generator=g, dtype=torch.int32).to(torch.int16)
+    fr[0, :, :] = -32768   # extreme products
+    fr[1, 0, :] = 32767
+    fr[1, 1, :] = -32768
+    out = _np(loc.correlate_prepared(fr.cuda().contiguous(), scores=True, grid=False))
+    for b in range(fr.shape[0]):
+        sc, best = oracle.xcorr(fr[b, 0].numpy(), fr[b, 1].numpy(), 46)
+        assert (out["scores"][b, 0] == sc).all(), b
+        assert out["lags"][b, 0] == best
+        assert (out["weighted"][b, 0] == oracle.prior(sc, best)).all()
+
+
+def test_ema_streams_vs_oracle(oracle):
+    loc = Localizer()
+    Sn, steps = 16, 24
+    rng = np.random.default_rng(21)
+    est = torch.zeros((Sn, 3, 93), dtype=torch.int64, device="cuda")
+    best = torch.zeros((Sn, 3), dtype=torch.int32, device="cuda")
+    est_ref = np.zeros((Sn, 3, 93), np.int64)
+    last = np.zeros(Sn, np.uint64)
+    lut = loc.lut()
+    for t in range(steps):
+        fresh = rng.integers(-(1 << 40), 1 << 40, (Sn, 3, 93)).astype(np.int64)
+        now = last + rng.integers(1000, 900000, Sn).astype(np.uint64)
+        dec = np.array([tdoa.decay_us(int(n), int(l)) for n, l in zip(now, last)], np.float32)
+        solve = {"cell": torch.empty(Sn, dtype=torch.int32, device="cuda"),
+                 "max_L": torch.empty(Sn, dtype=torch.int64, device="cuda"),
+                 "xy": torch.empty((Sn, 2), dtype=torch.float32, device="cuda")}
+        loc.average(est, torch.from_numpy(fresh).cuda(), torch.from_numpy(dec).cuda(), best, solve)
+        for s in range(Sn):
+            for p in range(3):
+                est_ref[s, p], b = oracle.average(est_ref[s, p], fresh[s, p], float(dec[s]))
+                assert best[s, p].item() == b
+            mL, cell = oracle.grid_solve(est_ref[s], lut.reshape(3, 101, 101))
+            assert solve["cell"][s].item() == cell and solve["max_L"][s].item() == mL
+        assert (est.cpu().numpy() == est_ref).all()
+        last = now
+
+
+def test_reference_symbols_gpu_backed(oracle):
+    """The reference-named per-frame entry points (tdoa_reference_abi.h)."""
+    L = tdoa.load()
+    g = golden("ref_components.npz")
+    win = golden("window_q15.npz")["n1024"]
+    # replay the ring, then write_out/normalize/window on the GPU
+    rb = _lib.RollingBuffer()
+    L.rolling_buffer_init(C.byref(rb))
+    k = 0
+    for i, v in enumerate(g["pushes"]):
+        L.rolling_buffer_push(C.byref(rb), int(v))
+        if i in list(g["snap_index"]):
+            b = _lib.Buffer()
+            L.rolling_buffer_write_out(C.byref(rb), C.byref(b))
+            assert (np.frombuffer(bytes(b.buffer), np.int16) == g["write_out"][k]).all()
+            assert b.power == g["write_out_power"][k]
+            L.buffer_normalize_range(C.byref(b))
+            assert (np.frombuffer(bytes(b.buffer), np.int16) == g["normalized"][k]).all()
+            L.buffer_window(C.byref(b))
+            assert (np.frombuffer(bytes(b.buffer), np.int16) == g["windowed"][k]).all()
+            k += 1
+    # correlations_init / correlations_average with a deterministic clock
+    clock = {"t": 5_000_000}
+
+    @_lib.CLOCK_FN
+    def now():
+        clock["t"] += 20_000
+        return clock["t"]
+
+    L.tdoa_ref_set_clock(now)
+    rng = np.random.default_rng(8)
+    est = _lib.Correlations()
+    est_ref = np.zeros(93, np.int64)
+    last = 0
+    for it in range(6):
+        a = oracle.window(oracle.normalize(oracle.dc_remove(rng.integers(0, 256, 1024))[0]), win)
+        d = int(rng.integers(-30, 31))
+        bsig = np.roll(a, d)
+        ba, bb = _lib.Buffer(), _lib.Buffer()
+        C.memmove(ba.buffer, a.ctypes.data, 2048)
+        C.memmove(bb.buffer, np.ascontiguousarray(bsig).ctypes.data, 2048)
+        new = _lib.Correlations()
+        L.correlations_init(C.byref(new), C.byref(ba), C.byref(bb))
+        sc, best = oracle.xcorr(a, bsig, 46)
+        assert new.best_shift == best
+        assert (np.frombuffer(bytes(new.correlations), np.int64) == oracle.prior(sc, best)).all()
+        L.correlations_average(C.byref(est), C.byref(new))
+        dec = oracle.decay(est.last_update, last)
+        est_ref, b = oracle.average(est_ref, oracle.prior(sc, best), dec)
+        last = est.last_update
+        assert (np.frombuffer(bytes(est.correlations), np.int64) == est_ref).all()
+        assert est.best_shift == b
+    L.tdoa_ref_set_clock(_lib.CLOCK_FN())

@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ fixtures (run in the build container, where
+/root/reference exists).  Outputs are DATA only -- no reference source text.
+
+  window_q15.npz          DPSS(N, NW=2) Q15 tables by the window.ipynb
+                          procedure (scipy), N = 256..4096
+  window_pins.json        sha256 of the reference's own window tables
+                          (window_function.h:5-70 for N=1024; the notebook's
+                          stored output window.ipynb:73-202 for N=2048) and
+                          whether the scipy tables equal them
+  ref_components.npz      inputs/outputs of the REFERENCE's buffer.c,
+                          rolling_buffer.c and microphones.c compiled
+                          unchanged (oracle/_ref): ring pushes + powers,
+                          write_out, normalize, window, mic positions
+  pipeline_cfg2.npz       64 ADC-like 3-mic x 1024 frames + 16 full-range
+                          frames and the oracle's outputs for the whole
+                          stateless path (xcorr stage: parity unpinned)
+  ema_sequence.npz        a 64-step correlations_average sequence (oracle)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "audio-triangulation_amd"))
+import oracle as O  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+REF = "/root/reference"
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.int32).tobytes()).hexdigest()
+
+
+def notebook_window(n: int) -> np.ndarray:
+    from scipy.signal import windows
+    w = windows.dpss(n, 2)          # window.ipynb cell 2
+    w /= np.max(w)
+    w /= np.max(np.abs(w))          # cell 3: to_int16
+    return np.round(w * 32767).astype(np.int32)
+
+
+def windows_fixture():
+    tabs = {f"n{n}": notebook_window(n) for n in (256, 512, 1024, 2048, 4096)}
+    np.savez_compressed(os.path.join(OUT, "window_q15.npz"), **tabs)
+    pins = {}
+    hdr = os.path.join(REF, "src/components/window_function.h")
+    txt = open(hdr).read()
+    body = txt[txt.index("{"):]
+    ref1024 = np.array([int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", body)], np.int32)
+    pins["window_function_h_1024_sha256"] = sha(ref1024)
+    pins["window_function_h_1024_equals_dpss"] = bool((ref1024 == tabs["n1024"]).all())
+    nb = json.load(open(os.path.join(REF, "window.ipynb")))
+    out_txt = "".join(nb["cells"][3]["outputs"][0]["text"])
+    m = re.search(r"window\[(\d+)\]", out_txt)
+    n_nb = int(m.group(1))
+    vals = np.array([int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", out_txt)], np.int32)
+    assert vals.size == n_nb
+    pins[f"notebook_output_{n_nb}_sha256"] = sha(vals)
+    pins[f"notebook_output_{n_nb}_equals_dpss"] = bool((vals == tabs[f"n{n_nb}"]).all())
+    for k, v in tabs.items():
+        pins[f"dpss_{k}_sha256"] = sha(v)
+    json.dump(pins, open(os.path.join(OUT, "window_pins.json"), "w"), indent=1, sort_keys=True)
+    return tabs, pins
+
+
+def ref_components_fixture(win1024):
+    R = O.ref()
+    assert R is not None, "oracle/_ref not built (make -C oracle)"
+    rng = np.random.default_rng(0x601DE4)
+    # ring: 3000 ADC-like pushes then 1500 full-range pushes
+    pushes = np.concatenate([rng.integers(0, 256, 3000), rng.integers(-32768, 32768, 1500)]).astype(np.int16)
+    rb = O.RefRollingBuffer()
+    R.rolling_buffer_init(C.byref(rb))
+    inc = np.zeros(pushes.size, np.int64)
+    outp = np.zeros(pushes.size, np.int64)
+    heads = np.zeros(pushes.size, np.int32)
+    snaps_at = [1023, 1500, 2999, 4499]
+    writeouts, wo_power, norm, winout, rings = [], [], [], [], []
+    for i, v in enumerate(pushes):
+        R.rolling_buffer_push(C.byref(rb), int(v))
+        inc[i] = R.rolling_buffer_get_incoming_power(C.byref(rb))
+        outp[i] = R.rolling_buffer_get_outgoing_power(C.byref(rb))
+        heads[i] = rb.head
+        if i in snaps_at:
+            rings.append(np.frombuffer(bytes(rb.buffer), np.int16).copy())
+            b = O.RefBuffer()
+            R.rolling_buffer_write_out(C.byref(rb), C.byref(b))
+            writeouts.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+            wo_power.append(b.power)
+            R.buffer_normalize_range(C.byref(b))
+            norm.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+            R.buffer_window(C.byref(b))
+            winout.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+    # direct buffer ops on full-range frames
+    fr = rng.integers(-32768, 32768, (8, 1024)).astype(np.int16)
+    fr_norm, fr_win = [], []
+    for row in fr:
+        b = O.RefBuffer()
+        C.memmove(b.buffer, row.ctypes.data, 2048)
+        R.buffer_normalize_range(C.byref(b))
+        fr_norm.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+        C.memmove(b.buffer, row.ctypes.data, 2048)
+        R.buffer_window(C.byref(b))
+        fr_win.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+    R.microphones_init()
+    mics = np.array([[O.RefPoint.in_dll(R, n).x, O.RefPoint.in_dll(R, n).y]
+                     for n in ("mic_a_location", "mic_b_location", "mic_c_location")], np.float32)
+    np.savez_compressed(
+        os.path.join(OUT, "ref_components.npz"),
+        pushes=pushes, incoming_power=inc, outgoing_power=outp, heads=heads,
+        snap_index=np.array(snaps_at), rings=np.array(rings), write_out=np.array(writeouts),
+        write_out_power=np.array(wo_power, np.int64), normalized=np.array(norm),
+        windowed=np.array(winout), frames=fr, frames_normalized=np.array(fr_norm),
+        frames_windowed=np.array(fr_win), mics=mics)
+    return mics
+
+
+def pipeline_fixture(win1024, mics):
+    import torch
+    from tdoa import synth
+    S = 46
+    lut = O.build_lut(mics, max_shift=S)
+    adc, cells, tau = synth.adc_frames(64, 3, 1024, lut, S, synth.SEEDS[2])
+    full = synth.full_range_frames(16, 3, 1024, 0xF011)
+    frames = torch.cat([adc, full]).numpy()
+    res = O.localize_batch(frames, S, win1024, lut)
+    np.savez_compressed(os.path.join(OUT, "pipeline_cfg2.npz"), frames=frames, lut=lut,
+                        cells=cells.numpy(), tau=tau.numpy(), **res)
+
+
+def ema_fixture():
+    rng = np.random.default_rng(0xE3A)
+    K, steps = 93, 64
+    fresh = rng.integers(-(1 << 40), 1 << 40, (steps, K)).astype(np.int64)
+    t = np.cumsum(rng.integers(1000, 400000, steps)).astype(np.uint64) + np.uint64(1_000_000)
+    est = np.zeros(K, np.int64)
+    last = 0
+    ests, bests, decays = [], [], []
+    for i in range(steps):
+        d = O.decay(int(t[i]), last)
+        est, b = O.average(est, fresh[i], d)
+        last = int(t[i])
+        ests.append(est.copy())
+        bests.append(b)
+        decays.append(d)
+    np.savez_compressed(os.path.join(OUT, "ema_sequence.npz"), fresh=fresh, t_us=t,
+                        est=np.array(ests), best=np.array(bests, np.int32),
+                        decay=np.array(decays, np.float32))
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    O.build()
+    tabs, pins = windows_fixture()
+    print("window pins:", {k: v for k, v in pins.items() if "equals" in k})
+    mics = ref_components_fixture(tabs["n1024"])
+    pipeline_fixture(tabs["n1024"], mics)
+    ema_fixture()
+    print("fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()
