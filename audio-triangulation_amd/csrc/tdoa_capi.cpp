@@ -203,6 +203,7 @@ struct tdoa_ctx {
     float *d_prior = nullptr;
     uint32_t *d_tuples = nullptr;
     int32_t *d_tuple_cell = nullptr;
+    float *d_tw = nullptr;  // GCC_PHAT twiddles: [N] e^{-2 pi i k/N}, then [N+1] e^{-2 pi i k/2N}
     tdoa_kparams kp;
 };
 
@@ -289,6 +290,8 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_prior);
     (void)hipFree(c->d_tuples);
     (void)hipFree(c->d_tuple_cell);
+    (void)hipFree(c->d_tw);
+    c->d_tw = nullptr;
     c->d_window = nullptr;
     c->d_prior = nullptr;
     c->d_tuples = nullptr;
@@ -314,7 +317,7 @@ extern "C" int tdoa_config_default(tdoa_config *cfg)
     cfg->grid_scale = 24.0f;
     cfg->height_offset = 1.2f;
     cfg->window_q15 = nullptr;
-    cfg->phat_eps = 1e-20f;
+    cfg->phat_eps = 1e-12f;
     return TDOA_OK;
 }
 
@@ -463,6 +466,29 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         delete c;
         return fail(TDOA_ERR_HIP, "uploading context tables: %s", hipGetErrorString(e));
     }
+    {
+        // GCC_PHAT twiddles, in double then rounded once
+        std::vector<float> tw(2 * N + 2 * (N + 1));
+        for (int k = 0; k < N; k++) {
+            const double a = -2.0 * M_PI * k / N;
+            tw[2 * k] = (float)std::cos(a);
+            tw[2 * k + 1] = (float)std::sin(a);
+        }
+        for (int k = 0; k <= N; k++) {
+            const double a = -2.0 * M_PI * k / (2.0 * N);
+            tw[2 * N + 2 * k] = (float)std::cos(a);
+            tw[2 * N + 2 * k + 1] = (float)std::sin(a);
+        }
+        if (hipMalloc(&c->d_tw, sizeof(float) * tw.size()) != hipSuccess ||
+            hipMemcpy(c->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice) !=
+                hipSuccess) {
+            free_device(c);
+            delete c;
+            return fail(TDOA_ERR_NOMEM, "uploading twiddle tables failed");
+        }
+        kp.tw = c->d_tw;
+        kp.tw2 = c->d_tw + 2 * N;
+    }
     kp.window = c->d_window;
     kp.prior = c->d_prior;
     kp.tuples = c->d_tuples;
@@ -518,14 +544,16 @@ static tdoa_kout to_kout(const tdoa_outputs *o)
 static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,
                      void *stream, bool prepared)
 {
-    if (!ctx || !out || (!frames && B > 0))
+    if (!ctx || !out)
         return fail(TDOA_ERR_INVALID, "localize: NULL argument");
     if (B < 0)
         return fail(TDOA_ERR_INVALID, "localize: negative batch");
-    if (!out->lags)
-        return fail(TDOA_ERR_INVALID, "localize: outputs.lags is required");
     if (B == 0)
         return TDOA_OK;
+    if (!frames)
+        return fail(TDOA_ERR_INVALID, "localize: NULL frames");
+    if (!out->lags)
+        return fail(TDOA_ERR_INVALID, "localize: outputs.lags is required");
     HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT && !prepared)
         return tdoa_launch_gcc_phat(ctx->kp, to_kout(out), frames, B, ctx->cfg.phat_eps, stream);

@@ -36,6 +36,8 @@ struct tdoa_kparams {
     const float *prior;        // [K] scale by |s - best|
     const uint32_t *tuples;    // [U][TW] packed lag indices (byte p = pair p)
     const int32_t *tuple_cell; // [U] first row-major cell of each tuple
+    const float *tw;           // GCC_PHAT: e^{-2 pi i k/N}, k < N   (re, im)
+    const float *tw2;          // GCC_PHAT: e^{-2 pi i k/2N}, k <= N (re, im)
 };
 
 struct tdoa_kout {

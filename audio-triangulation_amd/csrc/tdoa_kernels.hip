@@ -27,6 +27,22 @@
 
 int tdoa_set_error(int code, const char *msg);
 
+#ifdef TDOA_DIAG
+// Diagnostic build only (libtdoa_diag.so): per-workgroup phase stamps.
+#define TDOA_DIAG_SLOTS 8
+__device__ unsigned long long g_diag[1 << 20];
+#define DIAG_STAMP(i)                                                   \
+    do {                                                                \
+        if (threadIdx.x == 0)                                           \
+            g_diag[(size_t)blockIdx.x * TDOA_DIAG_SLOTS + (i)] =        \
+                __builtin_amdgcn_s_memtime();                           \
+    } while (0)
+#else
+#define DIAG_STAMP(i) \
+    do {              \
+    } while (0)
+#endif
+
 namespace {
 
 typedef short v2s __attribute__((ext_vector_type(2)));
@@ -95,7 +111,7 @@ __device__ __forceinline__ Smem carve(char *smem, const tdoa_kparams &kp, int nw
     o += (size_t)kp.F * kp.P * kp.K * 8;
     o = (o + 15) & ~(size_t)15;
     s.redv = (int64_t *)(smem + o);
-    o += (size_t)nwaves * 8;
+    o += (size_t)nwaves * 8 * 8;
     s.sums = (int *)(smem + o);
     o += (size_t)kp.F * kp.M * 4;
     s.best = (int *)(smem + o);
@@ -110,10 +126,10 @@ size_t smem_bytes(const tdoa_kparams &kp, int nwaves)
     o = (o + 15) & ~(size_t)15;
     o += (size_t)kp.F * kp.P * kp.K * 8;
     o = (o + 15) & ~(size_t)15;
-    o += (size_t)nwaves * 8;
+    o += (size_t)nwaves * 8 * 8;
     o += (size_t)kp.F * kp.M * 4;
     o += (size_t)kp.F * kp.P * 4;
-    o += (size_t)nwaves * 4;
+    o += (size_t)nwaves * 8 * 4;
     return (o + 15) & ~(size_t)15;
 }
 
@@ -270,25 +286,53 @@ __device__ void xcorr_phase(const tdoa_kparams &kp, const Smem &sm, int nf)
 }
 
 // -------------------------------------------------- argmax + lag prior + gate
-template <bool FLOATS>
-__device__ void argmax_prior_phase(const tdoa_kparams &kp, const Smem &sm, const tdoa_kout &out,
-                                   int64_t f0, int nf)
+// One wave per (frame, pair): first strictly-greater lag (correlations.c:20-23),
+// then weighted = score * scale[|s - best|] (correlations.c:26-33: for int64
+// scores (int64)((float)score * scale), truncating; float scores stay float).
+__device__ __forceinline__ void store_score(const tdoa_kout &o, size_t i, int64_t raw, int64_t w)
+{
+    if (o.scores)
+        o.scores[i] = raw;
+    if (o.weighted)
+        o.weighted[i] = w;
+}
+__device__ __forceinline__ void store_score(const tdoa_kout &o, size_t i, float raw, float w)
+{
+    if (o.scores_f)
+        o.scores_f[i] = raw;
+    if (o.weighted_f)
+        o.weighted_f[i] = w;
+}
+__device__ __forceinline__ int64_t apply_prior(int64_t v, float scale)
+{
+    const float x = (float)v * scale;
+    return (int64_t)x;
+}
+__device__ __forceinline__ float apply_prior(float v, float scale) { return v * scale; }
+
+template <typename T> __device__ __forceinline__ T lowest();
+template <> __device__ __forceinline__ int64_t lowest<int64_t>() { return INT64_MIN; }
+template <> __device__ __forceinline__ float lowest<float>() { return -INFINITY; }
+
+template <typename T>
+__device__ void argmax_prior_phase(const tdoa_kparams &kp, T *scores, int *bestlag,
+                                   const tdoa_kout &out, int64_t f0, int nf)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
     const int K = kp.K, P = kp.P;
     for (int fp = wave; fp < nf * P; fp += nwaves) {
-        int64_t *sc = sm.scores + fp * K;
+        T *sc = scores + fp * K;
         const int k1 = lane, k2 = lane + 64;
-        const int64_t v1 = k1 < K ? sc[k1] : INT64_MIN;
-        const int64_t v2 = k2 < K ? sc[k2] : INT64_MIN;
-        int64_t bv = v1;
+        const T v1 = k1 < K ? sc[k1] : lowest<T>();
+        const T v2 = k2 < K ? sc[k2] : lowest<T>();
+        T bv = v1;
         int bk = k1;
         if (v2 > bv) {
             bv = v2;
             bk = k2;
         }
         for (int m = 32; m >= 1; m >>= 1) {
-            const int64_t ov = __shfl_xor(bv, m, 64);
+            const T ov = __shfl_xor(bv, m, 64);
             const int ok = __shfl_xor(bk, m, 64);
             if (ov > bv || (ov == bv && ok < bk)) {
                 bv = ov;
@@ -296,31 +340,20 @@ __device__ void argmax_prior_phase(const tdoa_kparams &kp, const Smem &sm, const
             }
         }
         const size_t gbase = (size_t)(f0 * P + fp) * K;
-        if (out.scores) {
-            if (k1 < K)
-                out.scores[gbase + k1] = v1;
-            if (k2 < K)
-                out.scores[gbase + k2] = v2;
-        }
-        // correlations.c:27-32
         if (k1 < K) {
             const int d = k1 > bk ? k1 - bk : bk - k1;
-            const float x = (float)v1 * kp.prior[d];
-            const int64_t wv = (int64_t)x;
+            const T wv = apply_prior(v1, kp.prior[d]);
             sc[k1] = wv;
-            if (out.weighted)
-                out.weighted[gbase + k1] = wv;
+            store_score(out, gbase + k1, v1, wv);
         }
         if (k2 < K) {
             const int d = k2 > bk ? k2 - bk : bk - k2;
-            const float x = (float)v2 * kp.prior[d];
-            const int64_t wv = (int64_t)x;
+            const T wv = apply_prior(v2, kp.prior[d]);
             sc[k2] = wv;
-            if (out.weighted)
-                out.weighted[gbase + k2] = wv;
+            store_score(out, gbase + k2, v2, wv);
         }
         if (lane == 0) {
-            sm.best[fp] = bk - kp.S;
+            bestlag[fp] = bk - kp.S;
             out.lags[f0 * P + fp] = bk - kp.S;
         }
     }
@@ -329,7 +362,7 @@ __device__ void argmax_prior_phase(const tdoa_kparams &kp, const Smem &sm, const
         for (int f = tid; f < nf; f += blockDim.x) {
             int tot = 0;
             for (int p = 0; p < P; p++) {
-                const int b = sm.best[f * P + p];
+                const int b = bestlag[f * P + p];
                 tot += b * b;
             }
             out.gate[f0 + f] = tot > 4 ? 1 : 0;
@@ -338,67 +371,108 @@ __device__ void argmax_prior_phase(const tdoa_kparams &kp, const Smem &sm, const
 }
 
 // ------------------------------------------------------------- grid solve
+// All F frames of the workgroup in one sweep over the distinct lag tuples:
+// every tuple word is loaded once and scored for each frame, then one
+// (max L, first tuple) reduction per frame.  Tuples are in first-cell order,
+// so the smallest tuple index among the maxima carries the first row-major
+// argmax cell of vga_heatmap.h:99-108.
+#define TDOA_FMAX 8
+template <typename T>
+__device__ __forceinline__ void better(T &bv, int &bu, T ov, int ou)
+{
+    if (ov > bv || (ov == bv && ou < bu)) {
+        bv = ov;
+        bu = ou;
+    }
+}
+
+__device__ __forceinline__ void store_max(const tdoa_kout &o, int64_t i, int64_t v)
+{
+    if (o.max_L)
+        o.max_L[i] = v;
+}
+__device__ __forceinline__ void store_max(const tdoa_kout &o, int64_t i, float v)
+{
+    if (o.max_Lf)
+        o.max_Lf[i] = v;
+}
+
+template <typename T>
+__device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, int *redi,
+                             const tdoa_kout &out, int64_t f0, int nf)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const int K = kp.K, P = kp.P, TW = kp.TW, U = kp.U;
+    T bv[TDOA_FMAX];
+    int bu[TDOA_FMAX];
+#pragma unroll
+    for (int f = 0; f < TDOA_FMAX; f++) {
+        bv[f] = lowest<T>();
+        bu[f] = INT_MAX;
+    }
+    for (int u = tid; u < U; u += blockDim.x) {
+        T L[TDOA_FMAX];
+#pragma unroll
+        for (int f = 0; f < TDOA_FMAX; f++)
+            L[f] = 0;
+        for (int tw = 0; tw < TW; tw++) {
+            const uint32_t word = kp.tuples[u * TW + tw];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int p = 4 * tw + b;
+                if (p < P) {
+                    const int idx = p * K + ((word >> (8 * b)) & 0xFFu);
+#pragma unroll
+                    for (int f = 0; f < TDOA_FMAX; f++)
+                        if (f < nf)
+                            L[f] += scores[f * P * K + idx];
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < TDOA_FMAX; f++)
+            if (L[f] > bv[f]) {  // u increases per thread: strict > keeps the first
+                bv[f] = L[f];
+                bu[f] = u;
+            }
+    }
+#pragma unroll
+    for (int f = 0; f < TDOA_FMAX; f++) {
+        if (f < nf) {
+            for (int m = 32; m >= 1; m >>= 1)
+                better(bv[f], bu[f], __shfl_xor(bv[f], m, 64), __shfl_xor(bu[f], m, 64));
+            if (lane == 0) {
+                redv[wave * TDOA_FMAX + f] = bv[f];
+                redi[wave * TDOA_FMAX + f] = bu[f];
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < nf) {
+        const int f = tid;
+        T v = redv[f];
+        int ui = redi[f];
+        for (int w = 1; w < nwaves; w++)
+            better(v, ui, redv[w * TDOA_FMAX + f], redi[w * TDOA_FMAX + f]);
+        const int cell = kp.tuple_cell[ui];
+        const int64_t fi = f0 + f;
+        if (out.cell)
+            out.cell[fi] = cell;
+        store_max(out, fi, v);
+        if (out.xy) {
+            const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+            out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
+            out.xy[2 * fi + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+        }
+    }
+}
+
 __device__ void grid_phase(const tdoa_kparams &kp, const Smem &sm, const tdoa_kout &out,
                            int64_t f0, int nf)
 {
-    if (!out.cell && !out.xy && !out.max_L)
+    if (!out.cell && !out.xy && !out.max_L && !out.max_Lf)
         return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-    const int K = kp.K, P = kp.P, TW = kp.TW, U = kp.U;
-    for (int f = 0; f < nf; f++) {
-        const int64_t *Wt = sm.scores + f * P * K;
-        int64_t bv = INT64_MIN;
-        int bu = INT_MAX;
-        for (int u = tid; u < U; u += blockDim.x) {
-            int64_t L = 0;
-            for (int tw = 0; tw < TW; tw++) {
-                const uint32_t word = kp.tuples[u * TW + tw];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int p = 4 * tw + b;
-                    if (p < P)
-                        L += Wt[p * K + ((word >> (8 * b)) & 0xFFu)];
-                }
-            }
-            if (L > bv) {
-                bv = L;
-                bu = u;
-            }
-        }
-        for (int m = 32; m >= 1; m >>= 1) {
-            const int64_t ov = __shfl_xor(bv, m, 64);
-            const int ou = __shfl_xor(bu, m, 64);
-            if (ov > bv || (ov == bv && ou < bu)) {
-                bv = ov;
-                bu = ou;
-            }
-        }
-        if (lane == 0) {
-            sm.redv[wave] = bv;
-            sm.redi[wave] = bu;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < nwaves; w++) {
-                if (sm.redv[w] > bv || (sm.redv[w] == bv && sm.redi[w] < bu)) {
-                    bv = sm.redv[w];
-                    bu = sm.redi[w];
-                }
-            }
-            const int cell = kp.tuple_cell[bu];
-            const int64_t fi = f0 + f;
-            if (out.cell)
-                out.cell[fi] = cell;
-            if (out.max_L)
-                out.max_L[fi] = bv;
-            if (out.xy) {
-                const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
-                out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
-                out.xy[2 * fi + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
-            }
-        }
-        __syncthreads();
-    }
+    grid_phase_t<int64_t>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf);
 }
 
 template <bool PREPARED>
@@ -409,11 +483,16 @@ __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
     const int nf = (int)((B - f0) < kp.F ? (B - f0) : kp.F);
+    DIAG_STAMP(0);
     stage_frames<PREPARED>(kp, sm, frames, f0, nf);
+    DIAG_STAMP(1);
     xcorr_phase(kp, sm, nf);
-    argmax_prior_phase<false>(kp, sm, out, f0, nf);
+    DIAG_STAMP(2);
+    argmax_prior_phase<int64_t>(kp, sm.scores, sm.best, out, f0, nf);
     __syncthreads();
+    DIAG_STAMP(3);
     grid_phase(kp, sm, out, f0, nf);
+    DIAG_STAMP(4);
 }
 
 // --------------------------------------------------------------- EMA
@@ -561,6 +640,250 @@ __global__ void __launch_bounds__(256) k_ref_buffer(int op, int16_t *__restrict_
     }
 }
 
+// ================================================================ GCC-PHAT
+// One workgroup (N'/4 threads, N' = N) per frame.  With L = 2N (zero-padded
+// linear correlation) every mic's real FFT_L is one complex FFT_N' of
+// z[n] = x[2n] + i x[2n+1] (z = 0 for n >= N/2) plus a split step; every
+// pair's real inverse FFT_L is one complex inverse FFT_N' of
+// Y[k] = (R[k] + R*[N'-k]) + i (R[k] - R*[N'-k]) e^{+2 pi i k / L},
+// R = conj(X_i) X_j / max(|X_i^* X_j|, eps)   (PHAT),
+// y = IFFT(Y)/L  ->  r[2n] = Re y[n], r[2n+1] = Im y[n].
+// FFTs: Stockham autosort radix-4 (+ one radix-2 pass when log2 N' is odd)
+// in LDS, all M (then P) transforms of the frame advanced together.
+// Input samples are the same integer prep as DIRECT (DC, <<8, Q15 window),
+// scaled by 2^-15.
+
+struct cf {
+    float x, y;
+};
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ cf cconj(cf a) { return {a.x, -a.y}; }
+__device__ __forceinline__ cf mul_i(cf a) { return {-a.y, a.x}; }      // * i
+__device__ __forceinline__ cf mul_mi(cf a) { return {a.y, -a.x}; }    // * -i
+
+template <bool INV>
+__device__ __forceinline__ void fft4(cf &v0, cf &v1, cf &v2, cf &v3)
+{
+    const cf a = cadd(v0, v2), b = csub(v0, v2), c = cadd(v1, v3);
+    const cf d = INV ? mul_i(csub(v1, v3)) : mul_mi(csub(v1, v3));
+    v0 = cadd(a, c);
+    v1 = cadd(b, d);
+    v2 = csub(a, c);
+    v3 = csub(b, d);
+}
+
+__device__ __forceinline__ cf ldtw(const float *tw, int k) { return {tw[2 * k], tw[2 * k + 1]}; }
+
+// One Stockham radix-4 pass (Ns = size of finished sub-transforms) over nb
+// buffers of length n; every thread owns butterfly j = tid (n/4 threads).
+template <bool INV, int NB>
+__device__ void stockham4(cf *buf, int stride, int n, int Ns, const float *tw)
+{
+    const int j = threadIdx.x;
+    const int q = n >> 2;
+    const int k = j & (Ns - 1);
+    const int tstep = n / (4 * Ns);
+    cf w1 = ldtw(tw, k * tstep), w2 = ldtw(tw, 2 * k * tstep), w3 = ldtw(tw, 3 * k * tstep);
+    if (INV) {
+        w1 = cconj(w1);
+        w2 = cconj(w2);
+        w3 = cconj(w3);
+    }
+    cf v[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const cf *in = buf + b * stride;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            v[b][r] = in[j + r * q];
+    }
+    __syncthreads();
+    const int idxD = (j / Ns) * Ns * 4 + k;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        cf v0 = v[b][0], v1 = cmul(v[b][1], w1), v2 = cmul(v[b][2], w2), v3 = cmul(v[b][3], w3);
+        fft4<INV>(v0, v1, v2, v3);
+        cf *o = buf + b * stride;
+        o[idxD] = v0;
+        o[idxD + Ns] = v1;
+        o[idxD + 2 * Ns] = v2;
+        o[idxD + 3 * Ns] = v3;
+    }
+    __syncthreads();
+}
+
+// Final radix-2 pass (Ns = n/2): butterflies j and j + n/4 per thread.
+template <bool INV, int NB>
+__device__ void stockham2_last(cf *buf, int stride, int n, const float *tw)
+{
+    const int q = n >> 2, half = n >> 1;
+    cf v[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const cf *in = buf + b * stride;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int j = threadIdx.x + h * q;
+            v[b][2 * h] = in[j];
+            v[b][2 * h + 1] = in[j + half];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        cf *o = buf + b * stride;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int j = threadIdx.x + h * q;
+            cf w = ldtw(tw, j);
+            if (INV)
+                w = cconj(w);
+            const cf a = v[b][2 * h], c = cmul(v[b][2 * h + 1], w);
+            o[j] = cadd(a, c);
+            o[j + half] = csub(a, c);
+        }
+    }
+    __syncthreads();
+}
+
+template <bool INV, int NB>
+__device__ void fft_rest(cf *buf, int stride, int n, int Ns0, const float *tw)
+{
+    int Ns = Ns0;
+    for (; Ns * 4 <= n; Ns *= 4)
+        stockham4<INV, NB>(buf, stride, n, Ns, tw);
+    if (Ns < n)
+        stockham2_last<INV, NB>(buf, stride, n, tw);
+}
+
+template <int M>
+__global__ void __launch_bounds__(512) k_gcc_phat(tdoa_kparams kp, tdoa_kout out,
+                                                  const int16_t *__restrict__ frames, int64_t B,
+                                                  float eps2)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int P = M * (M - 1) / 2;
+    const int K = kp.K, N = kp.N;
+    const int n = N;           // complex FFT length N' (L = 2N)
+    const int tid = threadIdx.x;
+    // carve
+    size_t o = 0;
+    cf *C = (cf *)(smem + o);                       // [M][n]
+    o += (size_t)M * n * sizeof(cf);
+    Smem sm;
+    sm.X = (uint32_t *)(smem + o);                  // [M][N/2] staged words
+    o += (size_t)M * (N / 2) * 4;
+    float *scores = (float *)(smem + o);            // [P][K]
+    o += (size_t)P * K * 4;
+    o = (o + 15) & ~(size_t)15;
+    float *redv = (float *)(smem + o);              // [nwaves][FMAX] (8-byte slots)
+    o += (size_t)(blockDim.x >> 6) * TDOA_FMAX * 8;
+    int *redi = (int *)(smem + o);
+    o += (size_t)(blockDim.x >> 6) * TDOA_FMAX * 4;
+    sm.sums = (int *)(smem + o);
+    o += (size_t)M * 4;
+    int *bestlag = (int *)(smem + o);
+
+    const int64_t f0 = blockIdx.x;
+    {
+        tdoa_kparams k1 = kp;
+        k1.PADW = 0;
+        k1.RS = N / 2;
+        k1.F = 1;
+        stage_frames<false>(k1, sm, frames, f0, 1);
+    }
+    const float sc = 1.0f / 32768.0f;
+    // pass 1 (Ns = 1) straight from the staged words: inputs j, j+q nonzero,
+    // j+2q, j+3q are the zero padding.
+    {
+        const int j = tid, q = n >> 2;
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const uint32_t *xw = sm.X + m * (N / 2);
+            const uint32_t a = xw[j], b = xw[j + q];
+            const cf v0 = {(float)(int16_t)(a & 0xFFFFu) * sc, (float)(int16_t)(a >> 16) * sc};
+            const cf v1 = {(float)(int16_t)(b & 0xFFFFu) * sc, (float)(int16_t)(b >> 16) * sc};
+            cf *c = C + m * n + 4 * j;
+            c[0] = cadd(v0, v1);
+            c[1] = cadd(v0, mul_mi(v1));
+            c[2] = csub(v0, v1);
+            c[3] = cadd(v0, mul_i(v1));
+        }
+    }
+    __syncthreads();
+    fft_rest<false, M>(C, n, n, 4, kp.tw);
+
+    // split -> X_m[k], X_m[n-k]; PHAT cross spectra; inverse pre-twiddle into
+    // C[p] (bins are thread-private, so P <= M buffers are reused in place)
+    for (int k = tid; k <= n / 2; k += blockDim.x) {
+        const int kn = (n - k) & (n - 1);
+        cf Xk[M], Xn[M];
+        const cf w2k = ldtw(kp.tw2, k), w2n = ldtw(kp.tw2, n - k);
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const cf Zk = C[m * n + k], Zn = C[m * n + kn];
+            if (k == 0) {
+                Xk[m] = {Zk.x + Zk.y, 0.0f};      // X[0]
+                Xn[m] = {Zk.x - Zk.y, 0.0f};      // X[n] (Nyquist of L)
+            } else {
+                // X[k] = (Z[k] + Z*[n-k])/2 - i/2 w^k (Z[k] - Z*[n-k]),  w = e^{-2 pi i/L}
+                const cf e = cadd(Zk, cconj(Zn)), d = csub(Zk, cconj(Zn));
+                const cf od = cmul(w2k, d);
+                Xk[m] = {0.5f * (e.x + od.y), 0.5f * (e.y - od.x)};
+                const cf e2 = cadd(Zn, cconj(Zk)), d2 = csub(Zn, cconj(Zk));
+                const cf od2 = cmul(w2n, d2);
+                Xn[m] = {0.5f * (e2.x + od2.y), 0.5f * (e2.y - od2.x)};
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            // lexicographic pair p = (i, jj), compile-time after unrolling
+            int i = 0, jj = 1;
+            {
+                int q = p;
+                while (q >= M - 1 - i) {
+                    q -= M - 1 - i;
+                    i++;
+                }
+                jj = i + 1 + q;
+            }
+            cf Rk = cmul(cconj(Xk[i]), Xk[jj]);
+            cf Rn = cmul(cconj(Xn[i]), Xn[jj]);
+            const float ak = Rk.x * Rk.x + Rk.y * Rk.y, an = Rn.x * Rn.x + Rn.y * Rn.y;
+            const float rk = rsqrtf(fmaxf(ak, eps2)), rn = rsqrtf(fmaxf(an, eps2));
+            Rk = {Rk.x * rk, Rk.y * rk};
+            Rn = {Rn.x * rn, Rn.y * rn};
+            // Y[k] = (R[k] + R*[n-k]) + i (R[k] - R*[n-k]) conj(w^k)
+            const cf ae = cadd(Rk, cconj(Rn));
+            const cf ao = cmul(csub(Rk, cconj(Rn)), cconj(w2k));
+            C[p * n + k] = cadd(ae, mul_i(ao));
+            if (k != 0 && k != n / 2) {
+                const cf ae2 = cadd(Rn, cconj(Rk));
+                const cf ao2 = cmul(csub(Rn, cconj(Rk)), cconj(w2n));
+                C[p * n + kn] = cadd(ae2, mul_i(ao2));
+            }
+        }
+    }
+    __syncthreads();
+    fft_rest<true, P>(C, n, n, 1, kp.tw);
+
+    // lags -S..S of r = y/L: r[2u] = Re y[u], r[2u+1] = Im y[u]
+    const float invL = 1.0f / (float)(2 * n);
+    for (int i = tid; i < P * K; i += blockDim.x) {
+        const int p = i / K, s = i - p * K - kp.S;
+        const int m = s < 0 ? s + 2 * n : s;
+        const cf y = C[p * n + (m >> 1)];
+        scores[i] = ((m & 1) ? y.y : y.x) * invL;
+    }
+    __syncthreads();
+    argmax_prior_phase<float>(kp, scores, bestlag, out, f0, 1);
+    __syncthreads();
+    if (out.cell || out.xy || out.max_Lf)
+        grid_phase_t<float>(kp, scores, redv, redi, out, f0, 1);
+}
+
 int hip_fail(hipError_t e, const char *what)
 {
     char buf[256];
@@ -642,10 +965,40 @@ int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est, const i
     return 0;
 }
 
-int tdoa_launch_gcc_phat(const tdoa_kparams &, const tdoa_kout &, const int16_t *, int64_t, float,
-                         void *)
+int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
+                         int64_t B, float phat_eps, void *stream)
 {
-    return tdoa_set_error(-1, "GCC_PHAT engine not built yet");
+    if (((uintptr_t)frames & 15) != 0)
+        return tdoa_set_error(-1, "frames must be 16-byte aligned");
+    if (kp.P > kp.M)
+        return tdoa_set_error(-1, "GCC_PHAT: more pairs than mics (M > 3) not supported yet");
+    if (kp.N > 2048)
+        return tdoa_set_error(-1, "GCC_PHAT: frame_len > 2048 not supported yet");
+    if (!kp.tw || !kp.tw2)
+        return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
+    const int threads = kp.N / 4 < 64 ? 64 : kp.N / 4;
+    if (threads != kp.N / 4)
+        return tdoa_set_error(-1, "GCC_PHAT: frame_len must be >= 256");
+    const int nw = threads / 64;
+    size_t lds = (size_t)kp.M * kp.N * 8 + (size_t)kp.M * (kp.N / 2) * 4 + (size_t)kp.P * kp.K * 4;
+    lds = (lds + 15) & ~(size_t)15;
+    lds += (size_t)nw * TDOA_FMAX * 12 + (size_t)kp.M * 4 + (size_t)kp.P * 4 + 16;
+    if (lds > 160 * 1024)
+        return tdoa_set_error(-1, "GCC_PHAT: shape needs more than 160 KiB LDS");
+    if (B > INT_MAX)
+        return tdoa_set_error(-1, "GCC_PHAT: batch too large for one launch");
+    if (kp.M == 2)
+        hipLaunchKernelGGL(k_gcc_phat<2>, dim3((unsigned)B), dim3(threads), lds,
+                           (hipStream_t)stream, kp, out, frames, B, phat_eps * phat_eps);
+    else if (kp.M == 3)
+        hipLaunchKernelGGL(k_gcc_phat<3>, dim3((unsigned)B), dim3(threads), lds,
+                           (hipStream_t)stream, kp, out, frames, B, phat_eps * phat_eps);
+    else
+        return tdoa_set_error(-1, "GCC_PHAT: num_mics must be 2 or 3 for now");
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return hip_fail(e, "k_gcc_phat launch");
+    return 0;
 }
 
 int tdoa_launch_ref_buffer(int op, int16_t *buf, const int16_t *ring, int head, int64_t *power,
@@ -661,3 +1014,15 @@ int tdoa_launch_ref_buffer(int op, int16_t *buf, const int16_t *ring, int head, 
         return hip_fail(e, "k_ref_buffer launch");
     return 0;
 }
+
+#ifdef TDOA_DIAG
+extern "C" int tdoa_diag_fetch(unsigned long long *host, int n)
+{
+    if (n > (1 << 20))
+        n = 1 << 20;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif

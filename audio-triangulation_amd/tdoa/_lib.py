@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtdoa.so")
+LIB_PATH = os.environ.get("TDOA_LIB") or os.path.join(HERE, "libtdoa.so")
 
 ENGINE_DIRECT = 0
 ENGINE_GCC_PHAT = 1

@@ -78,7 +78,7 @@ typedef struct tdoa_config {
      * rounded (window.ipynb procedure; equals window_function.h at N=1024).
      * Copied. */
     const int32_t *window_q15;
-    float phat_eps;          /* GCC_PHAT: |cross| floor, default 1e-20f */
+    float phat_eps;          /* GCC_PHAT: floor of |X_i^* X_j| (samples scaled by 2^-15), default 1e-12 */
 } tdoa_config;
 
 /* Per-frame results (device pointers; any may be NULL unless noted). */

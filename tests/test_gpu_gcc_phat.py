@@ -1,0 +1,120 @@
+"""GCC_PHAT engine (fp32 FFT on gfx950) against the float64 oracle
+(oracle/gcc_phat_oracle.py).
+
+Tolerances (stated here, checked below):
+  scores_f, weighted_f   |gpu - fp64| <= 3e-5 absolute (PHAT scores lie in [-1, 1])
+  lags, gate             equal wherever the fp64 top-2 score margin > 2e-4
+  cell / xy              equal wherever the fp64 grid max beats every other
+                         tuple's L by > 1e-3 (xy is the cell's coordinates)
+  max_Lf                 |gpu - fp64| <= 1e-3
+On clean integer-delay frames the lags equal DIRECT's (the reference's).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+import gcc_phat_oracle as G  # noqa: E402
+from tdoa import synth  # noqa: E402
+from tdoa.localizer import Localizer  # noqa: E402
+
+TOL_SCORE = 3e-5
+TOL_LAG_MARGIN = 2e-4
+TOL_CELL_MARGIN = 1e-3
+
+
+def _np(d):
+    return {k: v.cpu().numpy() for k, v in d.items()}
+
+
+def check_phat(got, exp, grid=True):
+    s_exp = exp["scores_f"]
+    assert np.abs(got["scores_f"] - s_exp).max() <= TOL_SCORE
+    srt = np.sort(s_exp, axis=-1)
+    margin = srt[..., -1] - srt[..., -2]
+    sure = margin > TOL_LAG_MARGIN
+    assert (got["lags"][sure] == exp["lags"][sure]).all()
+    lag_ok = (got["lags"] == exp["lags"]).all(-1)
+    assert (got["gate"][lag_ok] == exp["gate"][lag_ok]).all()
+    same = got["lags"] == exp["lags"]
+    assert np.abs(got["weighted_f"] - exp["weighted_f"])[same].max(initial=0) <= TOL_SCORE
+    if grid:
+        Lg = exp["L"]
+        top = Lg.max(-1)
+        cells = got["cell"]
+        # margin of the fp64 max over every cell whose L differs from it
+        second = np.where(Lg >= top[:, None] - 1e-12, -np.inf, Lg).max(-1)
+        sure_c = (top - second > TOL_CELL_MARGIN) & lag_ok
+        Lsel = Lg[np.arange(len(cells)), cells]
+        assert (np.abs(Lsel[sure_c] - top[sure_c]) < 1e-9).all()
+        assert np.abs(got["max_Lf"] - exp["max_Lf"])[lag_ok].max(initial=0) <= 1e-3
+        W = 101
+        xy = np.stack([(cells % W - 50).astype(np.float32) / np.float32(24.0),
+                       (50 - cells // W).astype(np.float32) / np.float32(24.0)], -1)
+        assert (got["xy"] == xy).all()
+    return sure.mean()
+
+
+@pytest.fixture(scope="module")
+def phat3():
+    return Localizer(engine="gcc_phat")
+
+
+def test_golden_frames_vs_fp64(phat3):
+    g = golden("pipeline_cfg2.npz")
+    fr = torch.from_numpy(g["frames"]).cuda()
+    got = _np(phat3.localize(fr, scores=True))
+    exp = G.gcc_phat_batch(g["frames"], 46, phat3.window(), phat3.lut())
+    check_phat(got, exp)
+
+
+def test_cfg2_batch_vs_fp64_and_direct(phat3):
+    lut = phat3.lut().reshape(3, 101, 101)
+    fr, cells, tau = synth.adc_frames(4096, 3, 1024, lut, 46, synth.SEEDS[2], device="cuda")
+    got = _np(phat3.localize(fr, scores=True))
+    exp = G.gcc_phat_batch(fr.cpu().numpy(), 46, phat3.window(), lut)
+    frac_sure = check_phat(got, exp)
+    assert frac_sure > 0.95
+    # the north-star lag contract: on integer-delay frames GCC-PHAT lags match
+    # the injected delays and DIRECT's (the reference's) lags
+    direct = Localizer(engine="direct")
+    d = _np(direct.localize(fr))
+    assert (got["lags"][:, :2] == tau.cpu().numpy()[:, 1:]).mean() > 0.95
+    assert (got["lags"] == d["lags"]).mean() > 0.95
+
+
+def test_full_range_frames(phat3):
+    fr = synth.full_range_frames(256, 3, 1024, 0xBEE, device="cuda")
+    got = _np(phat3.localize(fr, scores=True))
+    exp = G.gcc_phat_batch(fr.cpu().numpy(), 46, phat3.window(), phat3.lut())
+    check_phat(got, exp)
+
+
+def test_constant_frames_tie_break(phat3):
+    fr = torch.full((3, 3, 1024), 77, dtype=torch.int16, device="cuda")
+    got = _np(phat3.localize(fr, scores=True))
+    assert (got["scores_f"] == 0).all() and (got["lags"] == -46).all()
+
+
+def test_empty_and_ragged(phat3):
+    out = phat3.localize(torch.empty((0, 3, 1024), dtype=torch.int16, device="cuda"))
+    assert out["lags"].shape == (0, 3)
+    lut = phat3.lut().reshape(3, 101, 101)
+    fr, _, _ = synth.adc_frames(5, 3, 1024, lut, 46, 3, device="cuda")
+    got = _np(phat3.localize(fr, scores=True))
+    check_phat(got, G.gcc_phat_batch(fr.cpu().numpy(), 46, phat3.window(), lut))
+
+
+@pytest.mark.parametrize("M,N,fs", [(2, 1024, 50000), (3, 256, 50000), (3, 512, 48000),
+                                    (3, 2048, 50000), (2, 2048, 48000)])
+def test_configs(M, N, fs):
+    mics = None if M == 3 else np.array([[-0.066, 0.0], [0.066, 0.0]], np.float32)
+    loc = Localizer(engine="gcc_phat", num_mics=M, frame_len=N, sample_rate_hz=fs, mic_xy=mics)
+    S = loc.dims.S
+    lut = loc.lut()
+    fr, _, _ = synth.adc_frames(96, M, N, lut, S, 40 + N, device="cuda")
+    got = _np(loc.localize(fr, scores=True))
+    check_phat(got, G.gcc_phat_batch(fr.cpu().numpy(), S, loc.window(), lut))

@@ -253,3 +253,27 @@ def test_ema_vs_numpy(oracle):
     exp = (est.astype(np.float32) + (fresh - est).astype(np.float32) * dec).astype(np.int64)
     got, best = oracle.average(est, fresh, float(dec))
     assert (got == exp).all() and best == int(np.argmax(exp)) - 46
+
+
+# ------------------------------------------------------- GCC-PHAT oracle
+def test_gcc_phat_prep_equals_c_oracle(oracle):
+    import gcc_phat_oracle as G
+    g = golden("pipeline_cfg2.npz")
+    win = golden("window_q15.npz")["n1024"]
+    fr = g["frames"][:20]
+    got = G.prep(fr, win)
+    for b in range(fr.shape[0]):
+        for m in range(3):
+            exp = oracle.window(oracle.normalize(oracle.dc_remove(fr[b, m])[0]), win)
+            assert (got[b, m] == exp).all()
+
+
+def test_gcc_phat_oracle_recovers_injected_delays():
+    import gcc_phat_oracle as G
+    g = golden("pipeline_cfg2.npz")
+    win = golden("window_q15.npz")["n1024"]
+    res = G.gcc_phat_batch(g["frames"][:64], 46, win, g["lut"])
+    # ADC-like frames: the (0,m) pairs peak at the injected delays, like DIRECT
+    agree = (res["lags"][:, :2] == g["tau"][:, 1:]).mean()
+    assert agree > 0.95
+    assert (res["lags"] == g["lags"][:64]).mean() > 0.9
