@@ -204,6 +204,10 @@ struct tdoa_ctx {
     uint32_t *d_tuples = nullptr;
     int32_t *d_tuple_cell = nullptr;
     float *d_tw = nullptr;  // GCC_PHAT twiddles: [N] e^{-2 pi i k/N}, then [N+1] e^{-2 pi i k/2N}
+    // weighted-score scratch for the grid kernel when the caller did not ask
+    // for weighted scores ([B][P][K] int64 or float); grows on demand
+    void *d_wscratch = nullptr;
+    size_t wscratch_bytes = 0;
     tdoa_kparams kp;
 };
 
@@ -291,6 +295,9 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_tuples);
     (void)hipFree(c->d_tuple_cell);
     (void)hipFree(c->d_tw);
+    (void)hipFree(c->d_wscratch);
+    c->d_wscratch = nullptr;
+    c->wscratch_bytes = 0;
     c->d_tw = nullptr;
     c->d_window = nullptr;
     c->d_prior = nullptr;
@@ -555,9 +562,33 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     if (!out->lags)
         return fail(TDOA_ERR_INVALID, "localize: outputs.lags is required");
     HIP_TRY(hipSetDevice(ctx->device));
-    if (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT && !prepared)
-        return tdoa_launch_gcc_phat(ctx->kp, to_kout(out), frames, B, ctx->cfg.phat_eps, stream);
-    return tdoa_launch_direct(ctx->kp, to_kout(out), frames, B, prepared, stream, nullptr);
+    const bool phat = ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT && !prepared;
+    tdoa_kout k = to_kout(out);
+    const bool grid = out->cell || out->xy || (phat ? out->max_Lf != nullptr : out->max_L != nullptr);
+    const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
+    if (grid && !weighted) {
+        // the grid kernel reads the weighted scores back: keep them in scratch
+        const size_t need = (size_t)B * ctx->P * ctx->K * (phat ? sizeof(float) : sizeof(int64_t));
+        if (need > ctx->wscratch_bytes) {
+            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+            (void)hipFree(ctx->d_wscratch);
+            ctx->d_wscratch = nullptr;
+            ctx->wscratch_bytes = 0;
+            if (hipMalloc(&ctx->d_wscratch, need) != hipSuccess)
+                return fail(TDOA_ERR_NOMEM, "weighted-score scratch of %zu bytes", need);
+            ctx->wscratch_bytes = need;
+        }
+        weighted = ctx->d_wscratch;
+        if (phat)
+            k.weighted_f = (float *)ctx->d_wscratch;
+        else
+            k.weighted = (int64_t *)ctx->d_wscratch;
+    }
+    int rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, stream)
+                  : tdoa_launch_direct(ctx->kp, k, frames, B, prepared, stream, nullptr);
+    if (rc != 0 || !grid)
+        return rc;
+    return tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
 }
 
 extern "C" int tdoa_localize_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B,

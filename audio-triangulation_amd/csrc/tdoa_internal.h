@@ -60,6 +60,8 @@ int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
 int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est,
                         const int64_t *fresh, const float *decay, int32_t *best,
                         const tdoa_kout *solve, void *stream);
+int tdoa_launch_grid(const tdoa_kparams &kp, const tdoa_kout &out, const void *weighted,
+                     bool is_float, int64_t B, void *stream);
 int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
                          const int16_t *frames, int64_t B, float phat_eps,
                          void *stream);

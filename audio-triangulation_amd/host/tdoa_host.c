@@ -43,7 +43,9 @@ static double urand(void)
 }
 static double nrand(void) { return sqrt(-2.0 * log(urand())) * cos(6.283185307179586 * urand()); }
 
-/* A quiet room, then a broadband burst reaching mic j delayed by tau[j]. */
+/* A quiet room, then a 700-sample broadband burst reaching mic j delayed by
+ * tau[j].  The reference's trigger (sample_compute.h:89) fires once the burst
+ * sits in the ring's older half and the newer half has gone quiet. */
 static void synth_samples(long t, const int tau[3], long burst_at, uint8_t out[3])
 {
     static double src[1 << 16];
@@ -54,9 +56,9 @@ static void synth_samples(long t, const int tau[3], long burst_at, uint8_t out[3
         init = 1;
     }
     for (int m = 0; m < 3; m++) {
-        double v = 128.0 + 3.0 * nrand();
+        double v = 128.0 + 0.5 * nrand();
         long u = t - tau[m] - burst_at;
-        if (u >= 0 && u < 4000)
+        if (u >= 0 && u < 700)
             v += 40.0 * src[u & 0xFFFF];
         v = v < 0 ? 0 : v > 255 ? 255 : v;
         out[m] = (uint8_t)lrint(v);

@@ -47,7 +47,7 @@ class Localizer:
                  engine: str = "direct", mic_xy=None, grid_half_w: int = 50,
                  grid_half_h: int = 50, grid_scale: float = 24.0,
                  height_offset: float = 1.2, speed_of_sound: float = 343.0,
-                 window_q15=None, phat_eps: float = 1e-20, device: int = 0):
+                 window_q15=None, phat_eps: float = 1e-12, device: int = 0):
         L = load()
         cfg = Config()
         L.tdoa_config_default(C.byref(cfg))

@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--also", action="store_true", help="also time the other engine")
+    ap.add_argument("--no-grid", action="store_true", help="diagnostic: skip the grid solve")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     return ap.parse_args()
 
@@ -66,7 +67,7 @@ def time_engine(engine, args, dev, rank, world, lut_cache):
         fr, _, _ = synth.adc_frames(B, M, N, lut, loc.dims.S,
                                     synth.SEEDS[2] + 7919 * rank + 104729 * r, device=dev)
         batches.append(fr)
-    out = loc.alloc_outputs(B)
+    out = loc.alloc_outputs(B, grid=not args.no_grid)
     stream = torch.cuda.current_stream(dev)
     for k in range(args.warmup):
         loc.localize_into(batches[k % R], out, stream)
