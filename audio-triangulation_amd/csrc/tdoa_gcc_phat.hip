@@ -366,8 +366,8 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
     const int K = kp.K, S = kp.S;
     f2 *bufs = (f2 *)smem;                      // [6][1024] FFT tiles / spectra
     f2 *twm = bufs + 6 * 1024;                  // [32][32] W_1024^{l*k}, swizzled
-    f2 *tw2s = twm + 1024;                      // [1025] W_2048^k
-    uint32_t *wins = (uint32_t *)(tw2s + 1026); // [512] Q15 window as int16 pairs
+    f2 *tw2s = twm + 1024;                      // [513] W_2048^k, k <= N/2
+    f2 *wins = tw2s + 514;                      // [512] Q15 window / 128, sample pairs
     int *bestlag = (int *)(wins + 512);         // [2][P]
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 31;
@@ -379,10 +379,11 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         const int l = e >> 5, k = e & 31;
         twm[swz(l, k)] = ldf2(kp.tw, (l * k) & (N - 1));
     }
-    for (int e = tid; e <= N; e += 192)
+    for (int e = tid; e <= N / 2; e += 192)
         tw2s[e] = ldf2(kp.tw2, e);
     for (int e = tid; e < 512; e += 192)
-        wins[e] = reinterpret_cast<const uint32_t *>(kp.window)[e];
+        wins[e] = f2{(float)kp.window[2 * e] * (1.0f / 128.0f),
+                     (float)kp.window[2 * e + 1] * (1.0f / 128.0f)};
     __syncthreads();
 
     const int64_t npairs = (B + 1) >> 1;
@@ -402,7 +403,6 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         }
     };
     fetch(blockIdx.x);
-    const float sc = 1.0f / 32768.0f;
     const float invL = 1.0f / 2048.0f;
 
 #ifdef TDOA_DIAG
@@ -423,7 +423,11 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         fetch(pair + gridDim.x);
 
         // ---- integer front end: floor-mean DC, <<8, Q15 window (rolling_buffer.c:64-66,
-        //      buffer.c:13-16, buffer.c:4-11) on words lane + 32 t of this mic row
+        //      buffer.c:13-16, buffer.c:4-11) on words lane + 32 t of this mic row.
+        //      Only the low byte of x - off survives `<<= 8`, so with s = sext8(x - off)
+        //      the windowed sample is ((s << 8) * W) >> 15 = floor(s * W / 128), an
+        //      integer below 2^23: exact in fp32 (wf holds W / 128).  Samples stay in
+        //      int16 units (PHAT is scale-invariant; eps2 is scaled to match).
         int s = 0;
 #pragma unroll
         for (int t = 0; t < 16; t++)
@@ -431,14 +435,18 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
 #pragma unroll
         for (int o = 16; o >= 1; o >>= 1)
             s += __shfl_xor(s, o, 64);
-        const uint32_t off16 = (uint32_t)(s >> 10) & 0xFFFFu;
+        const uint32_t off = (uint32_t)(s >> 10) & 0xFFu;
+        const uint32_t off2 = off | (off << 16);
         f2 v[32];
 #pragma unroll
         for (int t = 0; t < 16; t++) {
-            const int widx = lane + 32 * t;
-            const uint32_t wv = wins[widx];
-            const uint32_t p = prep_word(w[t], off16, wv);
-            v[t] = f2{(float)(int16_t)(p & 0xFFFFu) * sc, (float)(int16_t)(p >> 16) * sc};
+            // bit 8 set in each half: no borrow crosses into the high sample.  (Plain
+            // int8 casts: __builtin_amdgcn_sbfe on a masked word was converted as unsigned.)
+            const uint32_t d = (w[t] | 0x01000100u) - off2;
+            const float s0 = (float)(int8_t)(d & 0xFFu);
+            const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+            const f2 wf = wins[lane + 32 * t];
+            v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
         }
         // ---- forward FFT_1024 of z: lane = n2, v[n1] = z[n2 + 32 n1]
         fft32<false, true>(v);
@@ -464,41 +472,60 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         __syncthreads();
 
         PH_MARK(0);
-        // ---- split to X_m, PHAT cross spectra, inverse pre-twiddle (in place per bin pair)
-        for (int it = tid; it < 2 * 513; it += 192) {
-            const int f = it >= 513 ? 1 : 0;
-            const int k = it - 513 * f;
-            if (f >= nf)
-                continue;
-            const int kn = (N - k) & (N - 1);
-            f2 *fb = bufs + f * 3 * 1024;
-            const int ik = swz(k >> 5, k & 31), ikn = swz(kn >> 5, kn & 31);
-            const f2 w2k = tw2s[k], w2n = tw2s[N - k];
-            f2 Xk[M], Xn[M];
+        // ---- split to X_m, PHAT cross spectra, inverse pre-twiddle (in place per bin pair).
+        // Items it = tid + 192 r (2 frames x 513 bin pairs (k, N-k)), 3 per batch with all
+        // loads issued before any store.  The generic split is exact at k = 0 too
+        // (X[0] = Re + Im, X[N] = Re - Im with W_2048^N = -1), and the duplicate
+        // stores at k = 0 / N/2 write equal values.
 #pragma unroll
-            for (int m = 0; m < M; m++) {
-                const f2 Zk = fb[m * 1024 + ik], Zn = fb[m * 1024 + ikn];
-                if (k == 0) {
-                    Xk[m] = f2{Zk.x + Zk.y, 0.0f};
-                    Xn[m] = f2{Zk.x - Zk.y, 0.0f};
-                } else {
-                    const f2 e = Zk + conjf2(Zn), d = cmulf(w2k, Zk - conjf2(Zn));
-                    Xk[m] = 0.5f * f2{e.x + d.y, e.y - d.x};
-                    const f2 e2 = Zn + conjf2(Zk), d2 = cmulf(w2n, Zn - conjf2(Zk));
-                    Xn[m] = 0.5f * f2{e2.x + d2.y, e2.y - d2.x};
+        for (int r0 = 0; r0 < 6; r0 += 3) {
+            f2 Zk[3][M], Zn[3][M], w2[3];
+            int ik[3], ikn[3], fo[3];
+            bool live[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const int it = tid + 192 * (r0 + q);
+                const int f = it >= 513 ? 1 : 0;
+                const int k = it - 513 * f;
+                live[q] = it < 2 * 513 && f < nf;
+                const int kk = live[q] ? k : 0;
+                const int kn = (N - kk) & (N - 1);
+                fo[q] = (live[q] ? f : 0) * 3 * 1024;
+                ik[q] = swz(kk >> 5, kk & 31);
+                ikn[q] = swz(kn >> 5, kn & 31);
+                w2[q] = tw2s[kk];
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    Zk[q][m] = bufs[fo[q] + m * 1024 + ik[q]];
+                    Zn[q][m] = bufs[fo[q] + m * 1024 + ikn[q]];
                 }
             }
 #pragma unroll
-            for (int p = 0; p < P; p++) {
-                const int i = p < 2 ? 0 : 1, j = p == 0 ? 1 : 2;
-                f2 Rk = cmulf(conjf2(Xk[i]), Xk[j]);
-                f2 Rn = cmulf(conjf2(Xn[i]), Xn[j]);
-                Rk *= __builtin_amdgcn_rsqf(fmaxf(Rk.x * Rk.x + Rk.y * Rk.y, eps2));
-                Rn *= __builtin_amdgcn_rsqf(fmaxf(Rn.x * Rn.x + Rn.y * Rn.y, eps2));
-                fb[p * 1024 + ik] = (Rk + conjf2(Rn)) + times_i(cmulf(Rk - conjf2(Rn), conjf2(w2k)));
-                if (k != 0 && k != N / 2)
-                    fb[p * 1024 + ikn] =
-                        (Rn + conjf2(Rk)) + times_i(cmulf(Rn - conjf2(Rk), conjf2(w2n)));
+            for (int q = 0; q < 3; q++) {
+                const f2 w2k = w2[q], w2n = -conjf2(w2[q]);  // W_2048^{N-k} = -conj(W_2048^k)
+                f2 Xk[M], Xn[M];
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    const f2 a = Zk[q][m], b = Zn[q][m];
+                    const f2 e = a + conjf2(b), d = cmulf(w2k, a - conjf2(b));
+                    Xk[m] = 0.5f * f2{e.x + d.y, e.y - d.x};
+                    const f2 e2 = b + conjf2(a), d2 = cmulf(w2n, b - conjf2(a));
+                    Xn[m] = 0.5f * f2{e2.x + d2.y, e2.y - d2.x};
+                }
+                if (live[q]) {
+#pragma unroll
+                    for (int p = 0; p < P; p++) {
+                        const int i = p < 2 ? 0 : 1, j = p == 0 ? 1 : 2;
+                        f2 Rk = cmulf(conjf2(Xk[i]), Xk[j]);
+                        f2 Rn = cmulf(conjf2(Xn[i]), Xn[j]);
+                        Rk *= __builtin_amdgcn_rsqf(fmaxf(Rk.x * Rk.x + Rk.y * Rk.y, eps2));
+                        Rn *= __builtin_amdgcn_rsqf(fmaxf(Rn.x * Rn.x + Rn.y * Rn.y, eps2));
+                        bufs[fo[q] + p * 1024 + ik[q]] =
+                            (Rk + conjf2(Rn)) + times_i(cmulf(Rk - conjf2(Rn), conjf2(w2k)));
+                        bufs[fo[q] + p * 1024 + ikn[q]] =
+                            (Rn + conjf2(Rk)) + times_i(cmulf(Rn - conjf2(Rk), conjf2(w2n)));
+                    }
+                }
             }
         }
         __syncthreads();
@@ -610,7 +637,7 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
     hipStream_t st = (hipStream_t)stream;
     if (kp.M == 3 && kp.N == 1024 && kp.S <= 63) {
         // persistent 2-frame workgroups, as many as are resident at once
-        const size_t lds1024 = 7 * 1024 * 8 + 1026 * 8 + 512 * 4 + 8 * 4;
+        const size_t lds1024 = 7 * 1024 * 8 + 514 * 8 + 512 * 8 + 8 * 4;
         // resident workgroups for this LDS size (cached per device / size)
         static int c_dev = -1, c_resident = 0;
         static size_t c_lds = 0;
@@ -630,7 +657,7 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         const int64_t iters = (npairs + resident - 1) / resident;
         const int64_t grid = (npairs + iters - 1) / iters;
         hipLaunchKernelGGL(k_gcc_phat_1024, dim3((unsigned)grid), dim3(192), lds1024, st, kp, out,
-                           frames, B, eps2);
+                           frames, B, eps2 * 1152921504606846976.0f /* 2^60: int16 units */);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : hip_fail(e, "k_gcc_phat_1024 launch");
     }
