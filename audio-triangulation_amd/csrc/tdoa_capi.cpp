@@ -208,6 +208,10 @@ struct tdoa_ctx {
     // for weighted scores ([B][P][K] int64 or float); grows on demand
     void *d_wscratch = nullptr;
     size_t wscratch_bytes = 0;
+    // GCC_PHAT spectrum scratch for the two-pass shapes (M > 3 or N > 2048):
+    // a fixed chunk of frames' spectra that stays in L2 / MALL between passes
+    void *d_spec = nullptr;
+    size_t spec_bytes = 0;
     tdoa_kparams kp;
 };
 
@@ -296,6 +300,9 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_tuple_cell);
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_wscratch);
+    (void)hipFree(c->d_spec);
+    c->d_spec = nullptr;
+    c->spec_bytes = 0;
     c->d_wscratch = nullptr;
     c->wscratch_bytes = 0;
     c->d_tw = nullptr;
@@ -495,6 +502,15 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         }
         kp.tw = c->d_tw;
         kp.tw2 = c->d_tw + 2 * N;
+        if (tdoa_gcc_phat_needs_split(M, N)) {
+            const size_t want = (size_t)128 << 20;
+            if (hipMalloc(&c->d_spec, want) != hipSuccess) {
+                free_device(c);
+                delete c;
+                return fail(TDOA_ERR_NOMEM, "GCC_PHAT spectrum scratch of %zu bytes", want);
+            }
+            c->spec_bytes = want;
+        }
     }
     kp.window = c->d_window;
     kp.prior = c->d_prior;
@@ -584,7 +600,8 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
         else
             k.weighted = (int64_t *)ctx->d_wscratch;
     }
-    int rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, stream)
+    int rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, ctx->d_spec,
+                                         ctx->spec_bytes, stream)
                   : tdoa_launch_direct(ctx->kp, k, frames, B, prepared, stream, nullptr);
     if (rc != 0 || !grid)
         return rc;

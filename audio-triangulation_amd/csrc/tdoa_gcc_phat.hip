@@ -619,8 +619,11 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
 #endif
 }
 
+bool tdoa_gcc_phat_needs_split(int M, int N) { return M > 3 || N > 2048; }
+
 int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
-                         int64_t B, float phat_eps, void *stream)
+                         int64_t B, float phat_eps, void *spec_scratch, size_t spec_bytes,
+                         void *stream)
 {
     // |X_i^* X_j|^2 floor; kept a normal float (v_rsq_f32 flushes denormals)
     float eps2 = phat_eps * phat_eps;
@@ -628,12 +631,12 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         eps2 = 1e-30f;
     if (((uintptr_t)frames & 15) != 0)
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
-    if (kp.P > kp.M)
-        return tdoa_set_error(-1, "GCC_PHAT: more pairs than mics (M > 3) not supported yet");
-    if (kp.N > 2048)
-        return tdoa_set_error(-1, "GCC_PHAT: frame_len > 2048 not supported yet");
     if (!kp.tw || !kp.tw2)
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
+    if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
+        return tdoa_launch_gcc_phat_split(kp, out, frames, B,
+                                          eps2 * 1152921504606846976.0f /* 2^60: int16 units */,
+                                          spec_scratch, spec_bytes, stream);
     hipStream_t st = (hipStream_t)stream;
     if (kp.M == 3 && kp.N == 1024 && kp.S <= 63) {
         // persistent 2-frame workgroups, as many as are resident at once

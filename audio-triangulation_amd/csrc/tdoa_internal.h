@@ -2,6 +2,7 @@
 // and the gfx950 kernels (tdoa_kernels.hip).  Not part of the public ABI.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #define TDOA_MAX_PAIRS 28  // 8 mics
@@ -64,4 +65,10 @@ int tdoa_launch_grid(const tdoa_kparams &kp, const tdoa_kout &out, const void *w
                      bool is_float, int64_t B, void *stream);
 int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
                          const int16_t *frames, int64_t B, float phat_eps,
-                         void *stream);
+                         void *spec_scratch, size_t spec_bytes, void *stream);
+// GCC-PHAT shapes the fused kernels cannot hold (M > 3 or N > 2048): two
+// passes per chunk of frames through a spectrum scratch (tdoa_phat_split.hip)
+bool tdoa_gcc_phat_needs_split(int M, int N);
+int tdoa_launch_gcc_phat_split(const tdoa_kparams &kp, const tdoa_kout &out,
+                               const int16_t *frames, int64_t B, float eps2_int16,
+                               void *scratch, size_t scratch_bytes, void *stream);

@@ -35,13 +35,34 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
+
+# BASELINE.json configs 2-4 (per-GPU batch; config 4's 1e6 frames are 125000 per GPU at 8)
+CONFIGS = {
+    2: dict(desc="BASELINE config 2: 3-mic triangle, 1024-sample frames", M=3, N=1024,
+            mics=None, batch=4096),
+    3: dict(desc="BASELINE config 3: 4-mic square (0.15 m), 4096-sample frames, 6 pairs",
+            M=4, N=4096, mics="square", batch=65536),
+    4: dict(desc="BASELINE config 4: 8-mic circle (r 0.15 m), 2048-sample frames, 28 pairs",
+            M=8, N=2048, mics="circle", batch=125000),
+}
+
+
+def phat_flops(M, N):
+    """SURVEY.md 8(d) GCC-PHAT flop model per localization, L = 2N."""
+    import math
+    L, P = 2 * N, M * (M - 1) // 2
+    return M * 2.5 * L * math.log2(L) + P * 10 * (L / 2 + 1) + P * 2.5 * L * math.log2(L)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="default 400 (config 2), 20 otherwise")
+    ap.add_argument("--warmup", type=int, default=None, help="default 20 (config 2), 3 otherwise")
     ap.add_argument("--engine", default="gcc_phat", choices=["gcc_phat", "direct"])
-    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--rotate-mib", type=int, default=320,
                     help="frames rotated per rank (> 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -49,13 +70,32 @@ def parse():
     ap.add_argument("--also", action="store_true", help="also time the other engine")
     ap.add_argument("--no-grid", action="store_true", help="diagnostic: skip the grid solve")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    if a.batch is None:
+        a.batch = cfg["batch"]
+    if a.steps is None:
+        a.steps = 400 if a.config == 2 else 20
+    if a.warmup is None:
+        a.warmup = 20 if a.config == 2 else 3
+    return a
+
+
+def config_mics(cfg):
+    from tdoa import synth
+    if cfg["mics"] == "square":
+        return synth.square_mics(0.15)
+    if cfg["mics"] == "circle":
+        return synth.circle_mics(cfg["M"], 0.15)
+    return None
 
 
 def time_engine(engine, args, dev, rank, world, lut_cache):
     from tdoa import synth
     from tdoa.localizer import Localizer
-    loc = Localizer(engine=engine, device=dev.index)
+    cfg = CONFIGS[args.config]
+    loc = Localizer(engine=engine, num_mics=cfg["M"], frame_len=cfg["N"], mic_xy=config_mics(cfg),
+                    device=dev.index)
     M, N, P = loc.dims.M, loc.dims.N, loc.dims.P
     B = args.batch
     lut = loc.lut().reshape(P, 101, 101)
@@ -65,7 +105,8 @@ def time_engine(engine, args, dev, rank, world, lut_cache):
     batches = []
     for r in range(R):
         fr, _, _ = synth.adc_frames(B, M, N, lut, loc.dims.S,
-                                    synth.SEEDS[2] + 7919 * rank + 104729 * r, device=dev)
+                                    synth.SEEDS[args.config] + 7919 * rank + 104729 * r,
+                                    device=dev)
         batches.append(fr)
     out = loc.alloc_outputs(B, grid=not args.no_grid)
     stream = torch.cuda.current_stream(dev)
@@ -102,6 +143,7 @@ def time_engine(engine, args, dev, rank, world, lut_cache):
         "kernel_ms": kern_s * 1e3,
         "bytes_per_loc": bytes_per_loc,
         "achieved_gbs": bytes_per_loc * B / kern_s / 1e9,
+        "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
         "rotate_batches": R,
     }
     # sanity: outputs of the last step are finite / in range
@@ -115,17 +157,21 @@ def cpu_baseline(args, lut, window):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from tdoa import synth
+    cfg = CONFIGS[args.config]
+    M, N = cfg["M"], cfg["N"]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    fr, _, _ = synth.adc_frames(2048, 3, 1024, lut, 46, synth.SEEDS[2])
+    nfr = 2048 if args.config == 2 else 128
+    fr, _, _ = synth.adc_frames(nfr, M, N, lut, 46, synth.SEEDS[args.config])
     fr = fr.numpy()
-    O.localize_batch(fr[:64], 46, window, lut, threads=threads, want_scores=False)
+    O.localize_batch(fr[:16], 46, window, lut, threads=threads, want_scores=False)
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_seconds:
         O.localize_batch(fr, 46, window, lut, threads=threads, want_scores=False)
         n += fr.shape[0]
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "localizations/s", "cores": threads, "kind": "port",
-            "sample": f"{n} cfg2 frames (3x1024 ADC-like, batches of 2048) in {dt:.1f} s, "
+            "sample": f"{n} config-{args.config} frames ({M}x{N} ADC-like, batches of {nfr}) "
+                      f"in {dt:.1f} s, "
                       f"oracle/tdoa_oracle.c (reference correlations.c + vga_heatmap.h "
                       f"algorithm, DIRECT integer xcorr), OpenMP {threads} threads"}
 
@@ -148,16 +194,18 @@ def main():
                             rank, world, cache)
     if rank == 0:
         traffic = None
-        if os.path.exists(args.traffic_json):
+        if args.config == 2 and os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
                 traffic = tj.get(args.engine, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        cfg = CONFIGS[args.config]
+        shape = f"{cfg['M']}-mic x {cfg['N']}-sample frames"
         line = {
-            "metric": "GCC-PHAT localizations/sec, 3-mic x 1024-sample frames"
+            "metric": f"GCC-PHAT localizations/sec, {shape}"
             if args.engine == "gcc_phat" else
-            "localizations/sec (DIRECT exact xcorr), 3-mic x 1024-sample frames",
+            f"localizations/sec (DIRECT exact xcorr), {shape}",
             "value": main_res["value"],
             "unit": "localizations/s",
             "n_gpus": world,
@@ -170,16 +218,22 @@ def main():
             "dtype": "f32" if args.engine == "gcc_phat" else "int16->int64",
             "data": "synthetic (ADC-like u8 frames, injected integer delays, resident in HBM, "
                     f"{main_res['rotate_batches']} rotating batches > 256 MiB)",
-            "config": {"workload": "BASELINE config 2: 3-mic triangle, 1024-sample frames, "
-                                   f"batch {args.batch} per GPU, xcorr + lag prior + (x,y) grid",
-                       "engine": args.engine, "batch_per_gpu": args.batch, "mics": 3,
-                       "frame_len": 1024, "parallelism": f"dp{world} (frame shards, no collective)"},
+            "config": {"workload": f"{cfg['desc']}, batch {args.batch} per GPU, "
+                                   "xcorr + lag prior + (x,y) grid",
+                       "engine": args.engine, "batch_per_gpu": args.batch, "mics": cfg["M"],
+                       "frame_len": cfg["N"],
+                       "parallelism": f"dp{world} (frame shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": main_res["achieved_gbs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": main_res["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "kernel_ms": main_res["kernel_ms"],
                          "bytes_per_loc": main_res["bytes_per_loc"]},
+            # the bound that actually binds an fp32 FFT path: FP32 vector issue
+            "valu_roofline": {"achieved": main_res["valu_tflops"], "peak": VALU_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": main_res["valu_tflops"] / VALU_PEAK_TFLOPS,
+                              "flop_model": "SURVEY.md 8(d) GCC-PHAT model"}
+            if args.engine == "gcc_phat" else None,
             "cpu_baseline": None,
         }
         if other is not None:
