@@ -4,9 +4,10 @@
 // evaluated over the distinct lag tuples of the grid (tuples are in
 // first-cell order, so the first maximal tuple carries the first argmax cell).
 //
-// One 256-thread workgroup scores F = 8 frames per tuple: the tuple table
-// (U words) and the 8 frames' weighted scores, transposed to [p][k][frame],
-// sit in LDS, so one tuple costs P vector gathers for all 8 frames.
+// One workgroup scores GF = 8 frames per tuple (4 or 1 when their scores
+// would not fit): the tuple table (U x TW words, in chunks when large) and the
+// frames' weighted scores, transposed to [p][k][frame], sit in LDS, so one
+// tuple costs P vector gathers for all GF frames.
 // Running it apart from the FFT / xcorr kernels lets it run at full
 // occupancy; it reads B*P*K weighted scores (1.1 KiB/frame fp32) back from L2/HBM.
 
@@ -51,35 +52,31 @@ __device__ __forceinline__ void store_max_t<float>(const tdoa_kout &o, int64_t i
         o.max_Lf[i] = v;
 }
 
-// GF frames per workgroup (8; 1 for 8-mic grids whose scores fill LDS);
-// the tuple table is staged in LDS when it fits, else read from L2.
+// GF frames per workgroup (8, 4 or 1: as many as the [P][K][GF] score block
+// allows); the tuple table passes through LDS in chunks of CH tuples (one
+// chunk for 3-4 mic grids, several for the 28-pair grid of config 4).
 template <typename T, int TWC, int GF>
-__global__ void __launch_bounds__(256) k_grid(tdoa_kparams kp, tdoa_kout out,
-                                              const T *__restrict__ weighted, int64_t B,
-                                              int stage_tuples)
+__global__ void __launch_bounds__(1024) k_grid(tdoa_kparams kp, tdoa_kout out,
+                                               const T *__restrict__ weighted, int64_t B, int CH)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int P = kp.P, K = kp.K, U = kp.U, TW = kp.TW;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t *tups = stage_tuples ? (uint32_t *)smem : (uint32_t *)kp.tuples;  // [U * TW]
-    const size_t toff = stage_tuples ? ((((size_t)U * TW * 4) + 15) & ~(size_t)15) : 0;
-    T *W = (T *)(smem + toff);                                        // [P][K][GF]
-    T *redv = W + (size_t)P * K * GF;                                 // [4][GF]
-    int *redi = (int *)(redv + 4 * GF);                               // [4][GF]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nth = blockDim.x;
+    const int nwaves = nth >> 6;
+    uint32_t *tups = (uint32_t *)smem;                                      // [CH * TW]
+    T *W = (T *)(smem + ((((size_t)CH * TW * 4) + 15) & ~(size_t)15));      // [P][K][GF]
+    T *redv = W + (size_t)P * K * GF;                                       // [nwaves][GF]
+    int *redi = (int *)(redv + (size_t)nwaves * GF);                        // [nwaves][GF]
 
     const int64_t f0 = (int64_t)blockIdx.x * GF;
     const int nf = (B - f0) < GF ? (int)(B - f0) : GF;
-    if (stage_tuples)
-        for (int e = tid; e < U * TW; e += 256)
-            tups[e] = kp.tuples[e];
     // transpose the frames' [P][K] score rows to [p][k][frame]; absent frames
     // score the lowest value so they never matter
     const int PK = P * K;
-    for (int e = tid; e < GF * PK; e += 256) {
+    for (int e = tid; e < GF * PK; e += nth) {
         const int f = e / PK, r = e - f * PK;
         W[r * GF + f] = f < nf ? weighted[(f0 + f) * PK + r] : lowest_t<T>();
     }
-    __syncthreads();
 
     T bv[GF];
     int bu[GF];
@@ -88,33 +85,41 @@ __global__ void __launch_bounds__(256) k_grid(tdoa_kparams kp, tdoa_kout out,
         bv[f] = lowest_t<T>();
         bu[f] = INT_MAX;
     }
-    for (int u = tid; u < U; u += 256) {  // increasing u per thread: strict '>' keeps the first
-        T L[GF];
+    for (int c0 = 0; c0 < U; c0 += CH) {
+        const int n = (U - c0) < CH ? U - c0 : CH;
+        __syncthreads();  // previous chunk consumed (and, first time, W written)
+        for (int e = tid; e < n * TW; e += nth)
+            tups[e] = kp.tuples[(size_t)c0 * TW + e];
+        __syncthreads();
+        // increasing u per thread across chunks: strict '>' keeps the first
+        for (int u = tid; u < n; u += nth) {
+            T L[GF];
 #pragma unroll
-        for (int f = 0; f < GF; f++)
-            L[f] = 0;
+            for (int f = 0; f < GF; f++)
+                L[f] = 0;
 #pragma unroll
-        for (int tw = 0; tw < TWC; tw++) {
-            if (tw < TW) {
-                const uint32_t word = tups[u * TW + tw];
+            for (int tw = 0; tw < TWC; tw++) {
+                if (tw < TW) {
+                    const uint32_t word = tups[u * TW + tw];
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int p = 4 * tw + b;
-                    if (p < P) {
-                        const T *src = W + (size_t)(p * K + ((word >> (8 * b)) & 0xFFu)) * GF;
+                    for (int b = 0; b < 4; b++) {
+                        const int p = 4 * tw + b;
+                        if (p < P) {
+                            const T *src = W + (size_t)(p * K + ((word >> (8 * b)) & 0xFFu)) * GF;
 #pragma unroll
-                        for (int f = 0; f < GF; f++)
-                            L[f] += src[f];
+                            for (int f = 0; f < GF; f++)
+                                L[f] += src[f];
+                        }
                     }
                 }
             }
-        }
 #pragma unroll
-        for (int f = 0; f < GF; f++)
-            if (L[f] > bv[f]) {
-                bv[f] = L[f];
-                bu[f] = u;
-            }
+            for (int f = 0; f < GF; f++)
+                if (L[f] > bv[f]) {
+                    bv[f] = L[f];
+                    bu[f] = c0 + u;
+                }
+        }
     }
 #pragma unroll
     for (int f = 0; f < GF; f++) {
@@ -130,7 +135,7 @@ __global__ void __launch_bounds__(256) k_grid(tdoa_kparams kp, tdoa_kout out,
         const int f = tid;
         T v = redv[f];
         int ui = redi[f];
-        for (int w = 1; w < 4; w++)
+        for (int w = 1; w < nwaves; w++)
             better_t(v, ui, redv[w * GF + f], redi[w * GF + f]);
         if (ui < 0 || ui >= U)  // only if every L compared false (NaN scores)
             ui = 0;
@@ -154,35 +159,55 @@ int hip_fail(hipError_t e, const char *what)
     return tdoa_set_error(-2, buf);
 }
 
+template <typename T, int TWC>
+void launch_gf(int gf, dim3 grid, dim3 block, size_t lds, hipStream_t st, const tdoa_kparams &kp,
+               const tdoa_kout &out, const T *weighted, int64_t B, int CH)
+{
+    if (gf == 8)
+        hipLaunchKernelGGL((k_grid<T, TWC, 8>), grid, block, lds, st, kp, out, weighted, B, CH);
+    else if (gf == 4)
+        hipLaunchKernelGGL((k_grid<T, TWC, 4>), grid, block, lds, st, kp, out, weighted, B, CH);
+    else
+        hipLaunchKernelGGL((k_grid<T, TWC, 1>), grid, block, lds, st, kp, out, weighted, B, CH);
+}
+
 template <typename T>
 int launch(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
            void *stream)
 {
-    const size_t tbytes = (((size_t)kp.U * kp.TW * 4) + 15) & ~(size_t)15;
+    // frames per workgroup: the [P][K][GF] score block within 96 KiB
     const size_t per_frame = (size_t)kp.P * kp.K * sizeof(T);
-    const int gf = per_frame * 8 <= 48 * 1024 ? 8 : 1;
-    const size_t red = 4 * (size_t)gf * (sizeof(T) + sizeof(int));
-    const int stage = tbytes + per_frame * gf + red <= 96 * 1024 ? 1 : 0;
-    const size_t lds = (stage ? tbytes : 0) + per_frame * gf + red;
-    if (lds > 160 * 1024)
-        return tdoa_set_error(-1, "grid: scores of one frame exceed 160 KiB LDS");
+    int gf = 8;
+    while (gf > 1 && per_frame * gf > 96 * 1024)
+        gf /= 2;
+    if (gf == 2)
+        gf = 1;
+    // small grids (3-4 mics): 256 threads, several workgroups per CU; the
+    // 28-pair grid: one big workgroup per CU sharing one score block
+    const int threads = per_frame * gf > 32 * 1024 ? 1024 : 256;
+    const size_t red = (size_t)(threads / 64) * gf * (sizeof(T) + sizeof(int));
+    const size_t wbytes = per_frame * gf;
+    // tuple chunk: the whole table if it fits beside the scores, else what does
+    const size_t budget = 150 * 1024;
+    if (wbytes + red + 16 + (size_t)kp.TW * 4 * threads > budget)
+        return tdoa_set_error(-1, "grid: scores of one frame exceed the LDS budget");
+    size_t ch = (budget - wbytes - red - 16) / ((size_t)kp.TW * 4);
+    if (ch >= (size_t)kp.U)
+        ch = (size_t)kp.U;
+    else
+        ch = ch / threads * threads;
+    const int CH = (int)ch;
+    const size_t lds = ((((size_t)CH * kp.TW * 4) + 15) & ~(size_t)15) + wbytes + red;
     const int64_t grid = (B + gf - 1) / gf;
     if (grid > INT_MAX)
         return tdoa_set_error(-1, "grid: batch too large for one launch");
     hipStream_t st = (hipStream_t)stream;
     constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
-    if (kp.TW == 1 && gf == 8)
-        hipLaunchKernelGGL((k_grid<T, 1, 8>), dim3((unsigned)grid), dim3(256), lds, st, kp, out,
-                           weighted, B, stage);
-    else if (kp.TW == 1)
-        hipLaunchKernelGGL((k_grid<T, 1, 1>), dim3((unsigned)grid), dim3(256), lds, st, kp, out,
-                           weighted, B, stage);
-    else if (gf == 8)
-        hipLaunchKernelGGL((k_grid<T, TWX, 8>), dim3((unsigned)grid), dim3(256), lds, st, kp,
-                           out, weighted, B, stage);
+    if (kp.TW == 1)
+        launch_gf<T, 1>(gf, dim3((unsigned)grid), dim3(threads), lds, st, kp, out, weighted, B, CH);
     else
-        hipLaunchKernelGGL((k_grid<T, TWX, 1>), dim3((unsigned)grid), dim3(256), lds, st, kp,
-                           out, weighted, B, stage);
+        launch_gf<T, TWX>(gf, dim3((unsigned)grid), dim3(threads), lds, st, kp, out, weighted, B,
+                          CH);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "k_grid launch");
 }
