@@ -608,6 +608,12 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     return tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
 }
 
+// accessors for the streaming pipeline (tdoa_stream.cpp)
+const tdoa_kparams *tdoa_ctx_kparams(const tdoa_ctx *c) { return &c->kp; }
+int tdoa_ctx_device(const tdoa_ctx *c) { return c->device; }
+int tdoa_ctx_engine(const tdoa_ctx *c) { return c->cfg.engine; }
+int tdoa_ctx_rate(const tdoa_ctx *c) { return c->cfg.sample_rate_hz; }
+
 extern "C" int tdoa_localize_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B,
                                    const tdoa_outputs *out, void *stream)
 {

@@ -48,11 +48,18 @@ namespace {
 
 template <bool PREPARED, int TWC>
 __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
-                                                 const int16_t *__restrict__ frames, int64_t B)
+                                                 const int16_t *__restrict__ frames, int64_t B,
+                                                 const int32_t *__restrict__ count)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
+    if (count) {  // batch size known on the device only (streaming pipeline)
+        const int64_t c = *count;
+        B = c < B ? c : B;
+        if (f0 >= B)
+            return;
+    }
     const int nf = (int)((B - f0) < kp.F ? (B - f0) : kp.F);
     DIAG_STAMP(0);
     stage_frames<PREPARED>(kp, sm, frames, f0, nf);
@@ -248,7 +255,8 @@ static void direct_geometry(tdoa_kparams &kp, int &threads)
 }
 
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
-                       int64_t B, bool prepared, void *stream, int *lds_bytes_out)
+                       int64_t B, bool prepared, void *stream, int *lds_bytes_out,
+                       const int32_t *count_dev)
 {
     if (((uintptr_t)frames & 15) != 0)
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
@@ -266,7 +274,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
     hipStream_t st = (hipStream_t)stream;
 #define TDOA_LAUNCH_DIRECT(PREP, TWC)                                                       \
     hipLaunchKernelGGL((k_direct<PREP, TWC>), dim3((unsigned)grid), dim3(threads), lds, st, kp, \
-                       out, frames, B)
+                       out, frames, B, count_dev)
     if (kp.TW == 1) {
         if (prepared)
             TDOA_LAUNCH_DIRECT(true, 1);

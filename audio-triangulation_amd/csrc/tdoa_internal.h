@@ -54,10 +54,47 @@ struct tdoa_kout {
     float *weighted_f;
 };
 
-// Host-side launchers implemented in tdoa_kernels.hip.
+// Streaming state of one pipeline (tdoa_stream.hip); all device pointers.
+struct tdoa_stream_params {
+    int32_t M, N, H, log2N, fs;
+    int64_t capture_len;      // samples per stream in the capture ring
+    const uint8_t *capture;   // [S][capture_len][M] 8-bit ADC bytes, round-robin
+    int64_t *pos;             // [1] samples consumed (device clock)
+    int64_t *ring_start;      // [S] sample index of the last trigger (rings restart there)
+    int32_t *count;           // [1] frames triggered this step
+    int32_t *ids;             // [S] compact slot -> stream
+    int64_t *end;             // [S] samples consumed at the trigger
+    int16_t *frames;          // [S][M][N] triggered frames, compact
+    int64_t *fresh;           // [S][P][K] their weighted scores (k_direct)
+    int32_t *fresh_lags;      // [S][P]
+    uint8_t *fresh_gate;      // [S]
+    int64_t *est;             // [S][P][K] EMA scores per stream
+    uint64_t *last;           // [S] EMA clock per stream (us)
+    int64_t *stats;           // [2] running totals: triggered frames, gated frames
+};
+
+struct tdoa_stream_kout {
+    int32_t *count;
+    int32_t *stream_id;
+    int64_t *end;
+    int32_t *lags;
+    uint8_t *gate;
+    int32_t *ema_best;
+    int32_t *cell;
+    float *xy;
+    int64_t *max_L;
+};
+
+// Host-side launchers implemented in the .hip files.
+// count_dev (optional): device int32 batch size, B then only bounds the grid.
 int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
                        const int16_t *frames, int64_t B, bool prepared,
-                       void *stream, int *lds_bytes_out);
+                       void *stream, int *lds_bytes_out,
+                       const int32_t *count_dev = nullptr);
+size_t tdoa_stream_trigger_lds(int M, int N, int H);
+int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream);
+int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &kp,
+                              const tdoa_stream_kout &out, int64_t S, void *stream);
 int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est,
                         const int64_t *fresh, const float *decay, int32_t *best,
                         const tdoa_kout *solve, void *stream);

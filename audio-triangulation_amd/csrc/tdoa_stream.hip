@@ -1,0 +1,360 @@
+// tdoa_stream.hip -- the streaming loop of sample_compute.h:53-146 for S
+// independent mic-array streams, one hop of H samples per step (BASELINE
+// config 5).  Three kernels per step (plus k_direct on the triggered frames):
+//
+//   k_stream_trigger  one workgroup per stream: reads the hop's 8-bit ADC
+//                     bytes (dma_sampler.c:17-23, round-robin per mic, read
+//                     as sample_t at sample_compute.h:67-73) and the N-1
+//                     samples before it from the capture ring, evaluates the
+//                     trigger of sample_compute.h:75-91 after every sample of
+//                     the hop -- half powers of rolling_buffer.c:73-85 from
+//                     LDS prefix sums -- and takes the first firing sample
+//                     at least N samples after the stream's last trigger
+//                     (the rings restart empty after a trigger,
+//                     sample_compute.h:55-57).  A firing stream appends its
+//                     frame (the ring oldest..newest) to a compact batch.
+//   k_direct          (tdoa_direct.hip) on the compact batch, its size read
+//                     from device memory: write_out, normalize, window,
+//                     xcorr, prior, gate.
+//   k_stream_update   one workgroup per compact slot: for gated frames the
+//                     EMA of correlations.c:38-63 on the stream's state
+//                     (clock now_us = end * 1e6 / fs) and the grid solve on
+//                     the EMA scores (vga_heatmap.h:99-108 runs on corr_*);
+//                     advances the device sample clock by H.
+//
+// Built with -ffp-contract=off: the EMA's float steps round as the
+// reference's IEEE host build does.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+
+#include "tdoa_internal.h"
+
+int tdoa_set_error(int code, const char *msg);
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int MAX_CAND = 16;  // hop <= 4096 candidates, TPB per pass
+
+// inclusive block scan of per-thread totals (int32 and int64 together)
+__device__ __forceinline__ void block_exclusive_scan(int &v1, long long &v2, int *s1,
+                                                     long long *s2)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int x1 = v1;
+    long long x2 = v2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y1 = __shfl_up(x1, o, 64);
+        const long long y2 = __shfl_up(x2, o, 64);
+        if (lane >= o) {
+            x1 += y1;
+            x2 += y2;
+        }
+    }
+    if (lane == 63) {
+        s1[wave] = x1;
+        s2[wave] = x2;
+    }
+    __syncthreads();
+    int b1 = 0;
+    long long b2 = 0;
+    for (int w = 0; w < wave; w++) {
+        b1 += s1[w];
+        b2 += s2[w];
+    }
+    v1 = b1 + x1 - v1;  // exclusive
+    v2 = b2 + x2 - v2;
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(TPB) k_stream_trigger(tdoa_stream_params sp)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int M = sp.M, N = sp.N, H = sp.H, L = N + H - 1, tid = threadIdx.x;
+    int16_t *xs = (int16_t *)smem;                                   // [M][L]
+    size_t o = (((size_t)M * L * 2) + 15) & ~(size_t)15;
+    int *Q1 = (int *)(smem + o);                                      // [L + 1]
+    o += (((size_t)(L + 1) * 4) + 15) & ~(size_t)15;
+    long long *Q2 = (long long *)(smem + o);                          // [L + 1]
+    __shared__ int sc1[TPB / 64];
+    __shared__ long long sc2[TPB / 64];
+    __shared__ int first, slot;
+
+    const int64_t s = blockIdx.x;
+    const int64_t pos = *sp.pos;           // samples consumed before this hop
+    const int64_t base = pos + 1 - N;      // stream index of local sample 0
+    const uint8_t *cap = sp.capture + (size_t)s * sp.capture_len * M;
+    // local samples l = 0..L-1 <-> stream index base + l (zero before the stream starts)
+    {
+        int64_t j0 = base % sp.capture_len;
+        if (j0 < 0)
+            j0 += sp.capture_len;
+        for (int i = tid; i < L * M; i += TPB) {
+            const int l = i / M, m = i - l * M;
+            int64_t j = j0 + l;
+            if (j >= sp.capture_len)
+                j -= sp.capture_len;
+            xs[m * L + l] = base + l < 0 ? (int16_t)0 : (int16_t)cap[(size_t)j * M + m];
+        }
+    }
+    if (tid == 0)
+        first = INT_MAX;
+    __syncthreads();
+
+    // per candidate a (frame = local [a, a + N), end = pos + 1 + a): sum over
+    // mics of the outgoing (older half) and incoming (newer half) powers
+    const int hb = sp.log2N - 1;
+    long long pout[MAX_CAND], pin[MAX_CAND];
+#pragma unroll
+    for (int c = 0; c < MAX_CAND; c++)
+        pout[c] = pin[c] = 0;
+    const int per = (L + 1 + TPB - 1) / TPB;  // prefix entries per thread
+    for (int m = 0; m < M; m++) {
+        const int16_t *x = xs + m * L;
+        // Q[l] = sum_{l' < l} x, Q2 the same of x^2 (rolling_buffer.c:22-32 totals)
+        int t1 = 0;
+        long long t2 = 0;
+        const int l0 = tid * per;
+        for (int k = 0; k < per; k++) {
+            const int l = l0 + k;
+            if (l < L) {
+                const int v = x[l];
+                t1 += v;
+                t2 += (long long)v * v;
+            }
+        }
+        int e1 = t1;
+        long long e2 = t2;
+        block_exclusive_scan(e1, e2, sc1, sc2);
+        for (int k = 0; k <= per; k++) {
+            const int l = l0 + k;
+            if (l <= L && (k < per || l == L)) {
+                Q1[l] = e1;
+                Q2[l] = e2;
+            }
+            if (k < per && l < L) {
+                const int v = x[l];
+                e1 += v;
+                e2 += (long long)v * v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < MAX_CAND; c++) {
+            const int a = tid + TPB * c;
+            if (a < H) {
+                const int h = N >> 1;
+                const long long so1 = Q1[a + h] - Q1[a], so2 = Q2[a + h] - Q2[a];
+                const long long si1 = Q1[a + N] - Q1[a + h], si2 = Q2[a + N] - Q2[a + h];
+                pout[c] += (long long)((unsigned long long)so2 << hb) - so1 * so1;
+                pin[c] += (long long)((unsigned long long)si2 << hb) - si1 * si1;
+            }
+        }
+        __syncthreads();
+    }
+    const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
+    const int64_t rs = sp.ring_start[s];
+    // full ring: at least N samples since the last trigger
+    const int64_t amin = rs + N - pos - 1;
+#pragma unroll
+    for (int c = 0; c < MAX_CAND; c++) {
+        const int a = tid + TPB * c;
+        if (a < H && a >= amin && pout[c] > thr + pin[c]) {
+            atomicMin(&first, a);
+            break;  // candidates grow with c: this thread's first is its best
+        }
+    }
+    __syncthreads();
+    const int a = first;
+    if (a == INT_MAX)
+        return;
+    if (tid == 0) {
+        slot = atomicAdd(sp.count, 1);
+        const int64_t end = pos + 1 + a;
+        sp.ids[slot] = (int32_t)s;
+        sp.end[slot] = end;
+        sp.ring_start[s] = end;
+    }
+    __syncthreads();
+    int16_t *dst = sp.frames + (size_t)slot * M * N;
+    for (int i = tid; i < M * N; i += TPB) {
+        const int m = i / N, n = i - m * N;
+        dst[i] = xs[m * L + a + n];
+    }
+}
+
+// correlations.c:40-43 in the reference's float/double steps
+__device__ __forceinline__ float decay_us(uint64_t now, uint64_t last)
+{
+    const float dt = (float)(now - last) / 1e6f;
+    const float arg = -dt / 0.5f;
+    return (float)(1.0 - exp((double)arg));
+}
+
+__global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, tdoa_kparams kp,
+                                                       tdoa_stream_kout out)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int64_t *W = (int64_t *)smem;     // [P][K] EMA scores
+    __shared__ int64_t redv[TPB / 64];
+    __shared__ int redi[TPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = TPB / 64;
+    const int K = kp.K, P = kp.P;
+    const int slot = blockIdx.x;
+    const int cnt = *sp.count;
+    if (slot == 0 && tid == 0) {
+        *sp.pos += sp.H;  // every block of k_stream_trigger has read it
+        sp.stats[0] += cnt;
+        if (out.count)
+            *out.count = cnt;
+    }
+    if (slot >= cnt)
+        return;
+    const int s = sp.ids[slot];
+    if (out.lags) {
+        for (int p = tid; p < P; p += TPB)
+            out.lags[(size_t)slot * P + p] = sp.fresh_lags[(size_t)slot * P + p];
+    }
+    if (tid == 0) {
+        if (out.stream_id)
+            out.stream_id[slot] = s;
+        if (out.end)
+            out.end[slot] = sp.end[slot];
+        if (out.gate)
+            out.gate[slot] = sp.fresh_gate[slot];
+    }
+    if (!sp.fresh_gate[slot]) {  // sample_compute.h:134: only gated frames update
+        if (tid == 0) {
+            if (out.cell)
+                out.cell[slot] = -1;
+        }
+        return;
+    }
+    if (tid == 0)
+        atomicAdd((unsigned long long *)&sp.stats[1], 1ull);
+    const uint64_t now = (uint64_t)sp.end[slot] * 1000000u / (uint64_t)sp.fs;
+    const float dec = decay_us(now, sp.last[s]);
+    int64_t *est = sp.est + (size_t)s * P * K;
+    const int64_t *fr = sp.fresh + (size_t)slot * P * K;
+    for (int p = wave; p < P; p += nwaves) {
+        int64_t bv = INT64_MIN;
+        int bk = INT_MAX;
+        for (int k = lane; k < 128; k += 64) {
+            if (k < K) {
+                const int64_t ev = est[p * K + k];
+                const float delta = (float)(fr[p * K + k] - ev) * dec;
+                const float sum = (float)ev + delta;
+                const int64_t nv = (int64_t)sum;
+                est[p * K + k] = nv;
+                W[p * K + k] = nv;
+                if (nv > bv) {
+                    bv = nv;
+                    bk = k;
+                }
+            }
+        }
+        for (int m = 32; m >= 1; m >>= 1) {
+            const int64_t ov = __shfl_xor(bv, m, 64);
+            const int ok = __shfl_xor(bk, m, 64);
+            if (ov > bv || (ov == bv && ok < bk)) {
+                bv = ov;
+                bk = ok;
+            }
+        }
+        if (lane == 0 && out.ema_best)
+            out.ema_best[(size_t)slot * P + p] = bk - kp.S;
+    }
+    __syncthreads();
+    if (tid == 0)
+        sp.last[s] = now;
+    // grid solve on the EMA scores over the distinct lag tuples
+    int64_t bv = INT64_MIN;
+    int bu = INT_MAX;
+    for (int u = tid; u < kp.U; u += TPB) {
+        int64_t Lv = 0;
+        for (int tw = 0; tw < kp.TW; tw++) {
+            const uint32_t word = kp.tuples[u * kp.TW + tw];
+            for (int b = 0; b < 4; b++) {
+                const int p = 4 * tw + b;
+                if (p < P)
+                    Lv += W[p * K + ((word >> (8 * b)) & 0xFFu)];
+            }
+        }
+        if (Lv > bv) {
+            bv = Lv;
+            bu = u;
+        }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        const int64_t ov = __shfl_xor(bv, m, 64);
+        const int ou = __shfl_xor(bu, m, 64);
+        if (ov > bv || (ov == bv && ou < bu)) {
+            bv = ov;
+            bu = ou;
+        }
+    }
+    if (lane == 0) {
+        redv[wave] = bv;
+        redi[wave] = bu;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < nwaves; w++)
+            if (redv[w] > bv || (redv[w] == bv && redi[w] < bu)) {
+                bv = redv[w];
+                bu = redi[w];
+            }
+        if (bu < 0 || bu >= kp.U)
+            bu = 0;
+        const int cell = kp.tuple_cell[bu];
+        if (out.cell)
+            out.cell[slot] = cell;
+        if (out.max_L)
+            out.max_L[slot] = bv;
+        if (out.xy) {
+            const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+            out.xy[2 * slot] = (float)(cx - kp.half_w) / kp.grid_scale;
+            out.xy[2 * slot + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+        }
+    }
+}
+
+int fail_hip(hipError_t e, const char *what)
+{
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    return tdoa_set_error(-2, buf);
+}
+
+}  // namespace
+
+size_t tdoa_stream_trigger_lds(int M, int N, int H)
+{
+    const size_t L = (size_t)N + H - 1;
+    return ((M * L * 2 + 15) & ~(size_t)15) + (((L + 1) * 4 + 15) & ~(size_t)15) + (L + 1) * 8;
+}
+
+int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream)
+{
+    if (sp.H > TPB * MAX_CAND)
+        return tdoa_set_error(-1, "stream: hop too large");
+    const size_t lds = tdoa_stream_trigger_lds(sp.M, sp.N, sp.H);
+    if (lds > 150 * 1024)
+        return tdoa_set_error(-1, "stream: (frame_len + hop) x mics exceeds the LDS budget");
+    hipLaunchKernelGGL(k_stream_trigger, dim3((unsigned)S), dim3(TPB), lds, (hipStream_t)stream, sp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger launch");
+}
+
+int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &kp,
+                              const tdoa_stream_kout &out, int64_t S, void *stream)
+{
+    const size_t lds = (size_t)kp.P * kp.K * 8;
+    hipLaunchKernelGGL(k_stream_update, dim3((unsigned)S), dim3(TPB), lds, (hipStream_t)stream, sp,
+                       kp, out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail_hip(e, "k_stream_update launch");
+}

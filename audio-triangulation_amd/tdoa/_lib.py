@@ -27,6 +27,8 @@ EXPORTED_SYMBOLS = [
     "tdoa_localize_batch", "tdoa_correlate_prepared", "tdoa_average_batch",
     "tdoa_decay_us", "tdoa_get_window", "tdoa_get_mics", "tdoa_get_lut",
     "tdoa_get_prior", "tdoa_dpss_q15", "tdoa_last_error", "tdoa_abi_version",
+    "tdoa_stream_create", "tdoa_stream_step", "tdoa_stream_reset", "tdoa_stream_state",
+    "tdoa_stream_destroy",
     # tdoa_reference_abi.h
     "microphones_init", "rolling_buffer_init", "rolling_buffer_push",
     "rolling_buffer_write_out", "rolling_buffer_get_incoming_power",
@@ -61,6 +63,12 @@ class Outputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "lags", "gate", "cell", "xy", "max_L", "max_Lf", "scores", "weighted",
         "scores_f", "weighted_f")]
+
+
+class StreamOutputs(C.Structure):
+    """struct tdoa_stream_outputs (include/tdoa.h): device pointers."""
+    _fields_ = [(n, C.c_void_p) for n in (
+        "count", "stream_id", "end", "lags", "gate", "ema_best", "cell", "xy", "max_L")]
 
 
 # reference structs (include/tdoa_reference_abi.h, reference buffer.h:8-12,
@@ -115,6 +123,11 @@ def load() -> C.CDLL:
     L.tdoa_dpss_q15.argtypes = [I32, C.c_double, P]
     L.tdoa_last_error.restype = C.c_char_p
     L.tdoa_abi_version.restype = C.c_int
+    L.tdoa_stream_create.argtypes = [P, I32, I32, P, I64, C.c_int, C.POINTER(P)]
+    L.tdoa_stream_step.argtypes = [P, C.POINTER(StreamOutputs), P]
+    L.tdoa_stream_reset.argtypes = [P, P]
+    L.tdoa_stream_state.argtypes = [P, P, P, P, P]
+    L.tdoa_stream_destroy.argtypes = [P]
     # reference-named per-frame symbols
     L.microphones_init.argtypes = []
     L.rolling_buffer_init.argtypes = [C.POINTER(RollingBuffer)]

@@ -47,6 +47,45 @@ def full_range_frames(B: int, M: int, N: int, seed: int, device="cpu") -> torch.
                          dtype=torch.int32).to(torch.int16).contiguous()
 
 
+def adc_stream(S: int, T: int, M: int, lut: np.ndarray, max_shift: int, seed: int,
+               device: str | torch.device = "cpu", burst_len: int = 700,
+               gap: tuple = (1500, 3500), src_std: float = 40.0, noise_std: float = 0.5,
+               mean: float = 128.0) -> torch.Tensor:
+    """Config 5 capture bytes u8 [S][T][M] (round-robin per sample, dma_sampler.c:17-23).
+
+    Each stream has a stationary source at a random grid cell emitting
+    broadband bursts of `burst_len` samples separated by random gaps; mic m
+    hears it delayed by tau_m (the cell's LUT lags), over a quiet noise floor.
+    The reference triggers as a burst leaves the newer half of the ring."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    P, G = lut.shape[0], lut.reshape(lut.shape[0], -1).shape[1]
+    lut_t = torch.as_tensor(lut.reshape(P, -1).astype(np.int64), device=dev)
+    cells = torch.randint(0, G, (S,), generator=g, device=dev)
+    tau = torch.zeros((S, M), dtype=torch.int64, device=dev)
+    for m in range(1, M):
+        tau[:, m] = lut_t[m - 1][cells] - max_shift
+    pad = max_shift + 1
+    TT = T + 2 * pad
+    nb = TT // gap[0] + 2
+    gaps = torch.randint(gap[0], gap[1], (S, nb), generator=g, device=dev)
+    starts = torch.cumsum(gaps, 1) - gaps[:, :1] + torch.randint(0, gap[0], (S, 1), generator=g,
+                                                                 device=dev)
+    edge = torch.zeros((S, TT + burst_len + 1), dtype=torch.int32, device=dev)
+    ok = starts < TT
+    st = torch.where(ok, starts, torch.full_like(starts, TT))
+    edge.scatter_add_(1, st, ok.to(torch.int32))
+    edge.scatter_add_(1, st + burst_len, -ok.to(torch.int32))
+    env = (torch.cumsum(edge, 1)[:, :TT] > 0).to(torch.float32)
+    y = torch.randn((S, TT), generator=g, device=dev) * src_std * env
+    idx = torch.arange(T, device=dev).view(1, 1, T) + pad - tau.view(S, M, 1)
+    x = torch.gather(y.view(S, 1, -1).expand(S, M, -1), 2, idx)
+    x = x + torch.randn((S, M, T), generator=g, device=dev) * noise_std + mean
+    b = torch.clamp(torch.round(x), 0, 255).to(torch.uint8)
+    return b.permute(0, 2, 1).contiguous()
+
+
 def square_mics(side: float = 0.15) -> np.ndarray:
     """Config 3: 4-mic square centred on the origin."""
     h = side / 2

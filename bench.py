@@ -45,6 +45,10 @@ CONFIGS = {
             M=4, N=4096, mics="square", batch=65536),
     4: dict(desc="BASELINE config 4: 8-mic circle (r 0.15 m), 2048-sample frames, 28 pairs",
             M=8, N=2048, mics="circle", batch=125000),
+    # batch = streams per GPU; one step = one 512-sample hop of every stream
+    5: dict(desc="BASELINE config 5: streaming 48 kHz, 512-sample hop, 3-mic triangle, "
+                 "trigger + DIRECT xcorr + EMA + grid, one hipGraph per hop",
+            M=3, N=1024, mics=None, batch=16384, fs=48000, hop=512),
 }
 
 
@@ -58,8 +62,10 @@ def phat_flops(M, N):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 400 (config 2), 20 otherwise")
-    ap.add_argument("--warmup", type=int, default=None, help="default 20 (config 2), 3 otherwise")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="default 400 (config 2), 200 (config 5), 20 otherwise")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="default 20 (config 2, 5), 3 otherwise")
     ap.add_argument("--engine", default="gcc_phat", choices=["gcc_phat", "direct"])
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
@@ -75,9 +81,11 @@ def parse():
     if a.batch is None:
         a.batch = cfg["batch"]
     if a.steps is None:
-        a.steps = 400 if a.config == 2 else 20
+        a.steps = {2: 400, 5: 200}.get(a.config, 20)
     if a.warmup is None:
-        a.warmup = 20 if a.config == 2 else 3
+        a.warmup = 20 if a.config in (2, 5) else 3
+    if a.config == 5:
+        a.engine = "direct"  # the streaming loop runs the reference's DIRECT path
     return a
 
 
@@ -153,6 +161,79 @@ def time_engine(engine, args, dev, rank, world, lut_cache):
     return res
 
 
+def time_stream(args, dev, rank, world, cache):
+    """Config 5: S streams per GPU, capture ring resident in HBM (64 hops per
+    stream, replayed cyclically); a step = one hop of every stream."""
+    from tdoa import synth
+    from tdoa.localizer import Localizer
+    from tdoa.stream import StreamPipeline
+    cfg = CONFIGS[5]
+    loc = Localizer(sample_rate_hz=cfg["fs"], device=dev.index)
+    S, H = args.batch, cfg["hop"]
+    lut = loc.lut()
+    cache["lut"], cache["window"], cache["S"] = lut, loc.window(), loc.dims.S
+    T = 64 * H
+    cap = synth.adc_stream(S, T, 3, lut, loc.dims.S, synth.SEEDS[5] + 7919 * rank, device=dev)
+    torch.cuda.synchronize(dev)
+    pipe = StreamPipeline(loc, cap, hop=H, use_graph=True)
+    st = pipe.stream
+    for _ in range(args.warmup):
+        pipe.step()
+    st.synchronize()
+    _, trig0, gated0 = pipe.totals()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(st)
+    for _ in range(args.steps):
+        pipe.step()
+    ev1.record(st)
+    st.synchronize()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    _, trig1, gated1 = pipe.totals()
+    t = torch.tensor([wall, trig1 - trig0, gated1 - gated0], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t[0] = mx[0]
+    wall_max, trig, gated = float(t[0]), float(t[1]), float(t[2])
+    samples = world * S * H * args.steps
+    pipe.close()
+    return {"engine": "direct", "value": trig / wall_max, "ms_per_step": wall_max * 1e3 / args.steps,
+            "kernel_ms": gpu_s * 1e3 / args.steps, "triggered": trig, "gated": gated,
+            "stream_samples_per_s": samples / wall_max,
+            "realtime_streams": samples / wall_max / cfg["fs"],
+            "capture_bytes_per_step": world * S * H * 3}
+
+
+def cpu_baseline_stream(args, lut, window, S_lag):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from tdoa import synth
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    adc = synth.adc_stream(64, 64 * 512, 3, lut, S_lag, synth.SEEDS[5]).numpy()
+    O.stream_run(adc[:4, :4096], 1024, 48000, S_lag, window, lut, threads=threads)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        r = O.stream_run(adc, 1024, 48000, S_lag, window, lut, threads=threads, max_trig=64)
+        n += int(r["n_trig"].sum())
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "localizations/s", "cores": threads, "kind": "port",
+            "sample": f"{n} triggered frames from 64 streams x 32768 samples (config-5 capture "
+                      f"bytes) in {dt:.1f} s, oracle orc_stream_run (sample_compute.h:53-146 "
+                      f"sample by sample: rings, trigger, DIRECT xcorr, EMA, grid), OpenMP "
+                      f"{threads} threads over streams"}
+
+
 def cpu_baseline(args, lut, window):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -187,6 +268,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cache = {}
+    if args.config == 5:
+        return main_stream(args, dev, rank, world, cache)
     main_res = time_engine(args.engine, args, dev, rank, world, cache)
     other = None
     if args.also:
@@ -240,6 +323,37 @@ def main():
             line["other_engine"] = other
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args, cache["lut"], cache["window"])
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main_stream(args, dev, rank, world, cache):
+    res = time_stream(args, dev, rank, world, cache)
+    if rank == 0:
+        cfg = CONFIGS[5]
+        line = {
+            "metric": "streaming localizations/sec (triggered frames), 3-mic x 1024-sample "
+                      "frames, 48 kHz, 512-sample hop",
+            "value": res["value"], "unit": "localizations/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int16->int64",
+            "data": "synthetic u8 capture bytes (bursts from a fixed source per stream over a "
+                    "quiet floor), 64-hop capture ring per stream resident in HBM",
+            "config": {"workload": f"{cfg['desc']}, {args.batch} streams per GPU",
+                       "streams_per_gpu": args.batch, "hop": cfg["hop"], "fs": cfg["fs"],
+                       "mics": 3, "frame_len": 1024,
+                       "parallelism": f"dp{world} (stream shards, no collective)"},
+            "stream": {k: res[k] for k in ("kernel_ms", "triggered", "gated",
+                                           "stream_samples_per_s", "realtime_streams")},
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline_stream(args, cache["lut"], cache["window"],
+                                                       cache["S"])
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

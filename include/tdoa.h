@@ -141,6 +141,57 @@ int tdoa_get_prior(const tdoa_ctx *ctx, float *scale /* [K] by |d| */);
 /* DPSS(N, NW) first Slepian taper, Q15 as in window.ipynb. */
 int tdoa_dpss_q15(int32_t n, double nw, int32_t *out);
 
+/* ---- Streaming pipeline (sample_compute.h:53-146; BASELINE config 5) ----
+ * S independent mic-array streams whose 8-bit ADC bytes (dma_sampler.c:17-23:
+ * one u8 per mic, round-robin; read as sample_t at sample_compute.h:67-73)
+ * land in a device capture ring capture[S][capture_len][M].  Each
+ * tdoa_stream_step consumes the next `hop` samples of every stream:
+ *   trigger   after every sample, once N samples arrived since the stream's
+ *             last trigger (the rings restart empty, sample_compute.h:55-57),
+ *             fire when sum_m outgoing > 2 << 2(log2 N - 1) + sum_m incoming
+ *             (rolling_buffer.c:16-41,73-85; sample_compute.h:75-91), first
+ *             firing sample of the hop;
+ *   frame     the N samples before it through the DIRECT path (write_out,
+ *             normalize, window, xcorr, prior, gate);
+ *   EMA       gated frames only: correlations.c:38-63 on the stream's scores
+ *             with the clock now_us = end * 1e6 / fs (end = samples consumed
+ *             at the trigger; the EMA clock starts at 0 like corr_*'s static
+ *             zero init), then the grid solve on the EMA scores (the VGA
+ *             thread solves on corr_*, vga_heatmap.h:99-108).
+ * The step is a fixed kernel sequence reading its position from a device
+ * clock, so with use_graph it is captured once into a hipGraph and replayed.
+ * The producer keeps capture_len >= N + 2*hop samples of history per stream.
+ * Requires a DIRECT context; hop <= N. */
+typedef struct tdoa_stream tdoa_stream;
+
+typedef struct tdoa_stream_outputs { /* device pointers; slot order is arbitrary */
+    int32_t *count;     /* [1] frames triggered this step: slots 0..count-1 */
+    int32_t *stream_id; /* [S] stream of each slot                           */
+    int64_t *end;       /* [S] samples consumed at the trigger (frame = [end-N, end)) */
+    int32_t *lags;      /* [S][P] best lags of the fresh frame               */
+    uint8_t *gate;      /* [S] sum_p lag^2 > 4                               */
+    int32_t *ema_best;  /* [S][P] EMA best lags (gated slots)                */
+    int32_t *cell;      /* [S] grid argmax on the EMA scores; -1 if not gated */
+    float *xy;          /* [S][2] (gated slots)                              */
+    int64_t *max_L;     /* [S] (gated slots)                                 */
+} tdoa_stream_outputs;
+
+int tdoa_stream_create(tdoa_ctx *ctx, int32_t num_streams, int32_t hop,
+                       const uint8_t *capture, int64_t capture_len, int use_graph,
+                       tdoa_stream **out);
+/* One hop for every stream, asynchronous on `stream` (graph mode needs a
+ * non-NULL stream; the captured graph is reused while `out` and `stream`
+ * stay the same). */
+int tdoa_stream_step(tdoa_stream *st, const tdoa_stream_outputs *out, void *stream);
+/* Back to the start: position 0, rings empty, EMA scores 0, EMA clocks 0. */
+int tdoa_stream_reset(tdoa_stream *st, void *stream);
+/* Synchronous snapshot: samples consumed, EMA scores [S][P][K], EMA clocks
+ * [S] and running totals {triggered, gated} frames [2] (host pointers; any
+ * may be NULL). */
+int tdoa_stream_state(tdoa_stream *st, int64_t *pos, int64_t *est, uint64_t *last,
+                      int64_t *stats);
+int tdoa_stream_destroy(tdoa_stream *st);
+
 const char *tdoa_last_error(void);
 int tdoa_abi_version(void);
 

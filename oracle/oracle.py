@@ -55,6 +55,9 @@ def lib():
                                          P, P, C.c_int, C.c_int, C.c_float,
                                          C.c_int, C.c_int, P]
         L.orc_localize_batch.restype = C.c_int
+        L.orc_stream_run.argtypes = [P, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P]
+        L.orc_stream_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -76,6 +79,36 @@ class _BatchOut(C.Structure):
     _fields_ = [("scores", C.c_void_p), ("weighted", C.c_void_p),
                 ("lags", C.c_void_p), ("gate", C.c_void_p),
                 ("cell", C.c_void_p), ("max_L", C.c_void_p), ("xy", C.c_void_p)]
+
+
+class _StreamOut(C.Structure):
+    _fields_ = [("n_trig", C.c_void_p), ("end", C.c_void_p), ("lags", C.c_void_p),
+                ("gate", C.c_void_p), ("ema_best", C.c_void_p), ("cell", C.c_void_p),
+                ("max_L", C.c_void_p), ("est", C.c_void_p), ("last", C.c_void_p)]
+
+
+def stream_run(adc: np.ndarray, N: int, fs: int, max_shift: int, win: np.ndarray,
+               lut: np.ndarray | None, max_trig: int = 64, half_w=50, half_h=50, threads=0):
+    """sample_compute.h:53-146 over S streams of u8 ADC bytes [S][T][M].
+    Returns per-stream lists of trigger records plus the final EMA state."""
+    a = np.ascontiguousarray(adc, dtype=np.uint8)
+    S, T, M = a.shape
+    P, K = M * (M - 1) // 2, 2 * max_shift + 1
+    w = np.ascontiguousarray(win, dtype=np.int32)
+    r = {"n_trig": np.zeros(S, np.int32), "end": np.zeros((S, max_trig), np.int64),
+         "lags": np.zeros((S, max_trig, P), np.int32), "gate": np.zeros((S, max_trig), np.uint8),
+         "ema_best": np.zeros((S, max_trig, P), np.int32),
+         "cell": np.zeros((S, max_trig), np.int32), "max_L": np.zeros((S, max_trig), np.int64),
+         "est": np.zeros((S, P, K), np.int64), "last": np.zeros(S, np.uint64)}
+    o = _StreamOut(*[_p(r[k]).value for k in ("n_trig", "end", "lags", "gate", "ema_best",
+                                                "cell", "max_L", "est", "last")])
+    lut_c = np.ascontiguousarray(lut, dtype=np.uint8) if lut is not None else None
+    rc = lib().orc_stream_run(_p(a), S, T, M, N, fs, max_shift, _p(w),
+                              _p(lut_c) if lut_c is not None else None, half_w, half_h,
+                              max_trig, int(threads), C.byref(o))
+    if rc != 0:
+        raise ValueError("orc_stream_run rejected the shape")
+    return r
 
 
 # ---------------------------------------------------------------- stages

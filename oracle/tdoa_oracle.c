@@ -337,3 +337,111 @@ int orc_localize_batch(const int16_t *frames, int64_t B, int M, int N,
     }
     return 0;
 }
+
+/* sample_compute.h:53-146, one stream at a time (see tdoa_oracle.h). */
+int orc_stream_run(const uint8_t *adc, int64_t S, int64_t T, int M, int N, int fs,
+                   int max_shift, const int32_t *window, const uint8_t *lut, int half_w,
+                   int half_h, int max_trig, int threads, orc_stream_out *out)
+{
+    const int P = M * (M - 1) / 2, K = 2 * max_shift + 1;
+    const int W = 2 * half_w + 1, G = W * (2 * half_h + 1);
+    const int hb = ilog2(N) - 1;
+    const int64_t thr = (int64_t)2 << (2 * hb); /* POWER_THRESHOLD, sample_compute.h:21 */
+    if (M < 2 || M > 16 || N < 2 * K || (N & (N - 1)))
+        return -1;
+#ifdef _OPENMP
+    if (threads > 0)
+        omp_set_num_threads(threads);
+#pragma omp parallel
+#endif
+    {
+        int16_t *store = (int16_t *)malloc((size_t)M * N * sizeof(int16_t));
+        int16_t *x = (int16_t *)malloc((size_t)M * N * sizeof(int16_t));
+        int64_t *sc = (int64_t *)malloc((size_t)P * K * sizeof(int64_t));
+        int64_t *est = (int64_t *)malloc((size_t)P * K * sizeof(int64_t));
+        int32_t *bst = (int32_t *)malloc((size_t)P * sizeof(int32_t));
+        orc_ring *rb = (orc_ring *)malloc((size_t)M * sizeof(orc_ring));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t s = 0; s < S; s++) {
+            const uint8_t *a = adc + (size_t)s * T * M;
+            int nt = 0;
+            uint64_t last = 0;
+            memset(est, 0, (size_t)P * K * sizeof(int64_t));
+            for (int m = 0; m < M; m++)
+                orc_ring_init(&rb[m], store + (size_t)m * N, N);
+            for (int64_t t = 0; t < T; t++) {
+                int full = 1;
+                for (int m = 0; m < M; m++) {
+                    orc_ring_push(&rb[m], (int16_t)a[(size_t)t * M + m]);
+                    full &= rb[m].is_full;
+                }
+                if (!full)
+                    continue;
+                int64_t po = 0, pi = 0;
+                for (int m = 0; m < M; m++) {
+                    po += orc_ring_outgoing_power(&rb[m]);
+                    pi += orc_ring_incoming_power(&rb[m]);
+                }
+                if (!(po > thr + pi))
+                    continue;
+                /* triggered after sample t: the frame ends at t + 1 */
+                const int64_t end = t + 1;
+                const uint64_t now = (uint64_t)end * 1000000u / (uint64_t)fs;
+                int gate = 0;
+                for (int m = 0; m < M; m++) {
+                    int16_t *xm = x + (size_t)m * N;
+                    orc_ring_write_out(&rb[m], xm, NULL);
+                    orc_normalize(xm, N);
+                    orc_window(xm, window, N);
+                }
+                const size_t r = (size_t)s * max_trig + nt;
+                int p = 0;
+                for (int i = 0; i < M; i++)
+                    for (int j = i + 1; j < M; j++, p++) {
+                        int32_t b;
+                        orc_xcorr(x + (size_t)i * N, x + (size_t)j * N, N, max_shift,
+                                  sc + (size_t)p * K, &b);
+                        orc_prior(sc + (size_t)p * K, max_shift, b);
+                        if (nt < max_trig)
+                            out->lags[r * P + p] = b;
+                        gate += b * b;
+                    }
+                int32_t cell = -1;
+                int64_t mL = 0;
+                if (gate > 4) {
+                    const float decay = orc_decay(now, last);
+                    for (p = 0; p < P; p++)
+                        orc_average(est + (size_t)p * K, sc + (size_t)p * K, K, decay, &bst[p]);
+                    last = now;
+                    if (lut)
+                        orc_grid_solve(est, P, K, lut, G, &mL, &cell);
+                }
+                if (nt < max_trig) {
+                    out->end[r] = end;
+                    out->gate[r] = gate > 4;
+                    for (p = 0; p < P; p++)
+                        out->ema_best[r * P + p] = gate > 4 ? bst[p] : 0;
+                    out->cell[r] = cell;
+                    out->max_L[r] = mL;
+                }
+                nt++;
+                for (int m = 0; m < M; m++) /* sample_compute.h:55-57 */
+                    orc_ring_init(&rb[m], store + (size_t)m * N, N);
+            }
+            out->n_trig[s] = nt;
+            if (out->est)
+                memcpy(out->est + (size_t)s * P * K, est, (size_t)P * K * sizeof(int64_t));
+            if (out->last)
+                out->last[s] = last;
+        }
+        free(store);
+        free(x);
+        free(sc);
+        free(est);
+        free(bst);
+        free(rb);
+    }
+    return 0;
+}

@@ -101,6 +101,33 @@ int orc_localize_batch(const int16_t *frames /* [B][M][N] raw */, int64_t B,
                        float grid_scale, int do_grid, int threads,
                        orc_batch_out *out);
 
+/* ---- a13 + a9 + a12 streaming: sample_compute.h:53-146 for S independent
+ *      streams, driven sample by sample from 8-bit round-robin ADC bytes
+ *      (dma_sampler.c:17-23, sample_compute.h:67-73).  Per stream: rings
+ *      restart empty; after every pushed sample, once full, trigger when
+ *      sum_m outgoing > (2 << 2*(log2 N - 1)) + sum_m incoming; the frame
+ *      (ring oldest..newest) runs write_out -> normalize -> window -> xcorr
+ *      -> prior -> gate; gated frames update the EMA (correlations.c:38-63,
+ *      clock now_us = end * 1e6 / fs, end = samples consumed, EMA last = 0
+ *      at start) and the grid solve runs on the EMA scores (vga_heatmap.h:
+ *      99-108, the VGA thread's corr_*).  Records per trigger, in order. ---- */
+typedef struct orc_stream_out {
+    int32_t *n_trig;   /* [S] */
+    int64_t *end;      /* [S][max_trig] samples consumed at the trigger */
+    int32_t *lags;     /* [S][max_trig][P] fresh best lags */
+    uint8_t *gate;     /* [S][max_trig] */
+    int32_t *ema_best; /* [S][max_trig][P] EMA best lags (gated; else 0) */
+    int32_t *cell;     /* [S][max_trig] grid argmax on EMA (gated; else -1) */
+    int64_t *max_L;    /* [S][max_trig] */
+    int64_t *est;      /* [S][P][K] final EMA state, may be NULL */
+    uint64_t *last;    /* [S] final EMA clock, may be NULL */
+} orc_stream_out;
+
+int orc_stream_run(const uint8_t *adc /* [S][T][M] */, int64_t S, int64_t T, int M,
+                   int N, int fs, int max_shift, const int32_t *window,
+                   const uint8_t *lut, int half_w, int half_h, int max_trig,
+                   int threads, orc_stream_out *out);
+
 #ifdef __cplusplus
 }
 #endif

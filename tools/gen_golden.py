@@ -16,6 +16,15 @@
                           frames and the oracle's outputs for the whole
                           stateless path (xcorr stage: parity unpinned)
   ema_sequence.npz        a 64-step correlations_average sequence (oracle)
+  stream_trace.npz        config-5 style capture bytes (3 streams x 12000
+                          samples x 3 mics, 48 kHz) driven sample by sample
+                          through the REFERENCE's rolling_buffer.c /
+                          buffer.c (oracle/_ref) as sample_compute.h:53-118
+                          does: trigger ends and the prepared frames; plus
+                          the oracle's xcorr / EMA / grid records for them
+
+    python tools/gen_golden.py            # all fixtures
+    python tools/gen_golden.py stream     # only stream_trace.npz
 """
 from __future__ import annotations
 
@@ -158,14 +167,61 @@ def ema_fixture():
                         decay=np.array(decays, np.float32))
 
 
+def stream_fixture(win1024, mics):
+    """sample_compute.h:53-118 with the reference's own ring / buffer code."""
+    from tdoa import synth
+    R = O.ref()
+    assert R is not None, "oracle/_ref not built (make -C oracle)"
+    fs, N, S_lag = 48000, 1024, 44
+    lut = O.build_lut(mics, fs=fs, max_shift=S_lag)
+    adc = synth.adc_stream(3, 12000, 3, lut, S_lag, synth.SEEDS[5]).numpy()
+    thr = 2 << 18  # POWER_THRESHOLD at N = 1024
+    ends, frames = [], []
+    for s in range(adc.shape[0]):
+        rb = [O.RefRollingBuffer() for _ in range(3)]
+        for r in rb:
+            R.rolling_buffer_init(C.byref(r))
+        for t in range(adc.shape[1]):
+            for m in range(3):
+                R.rolling_buffer_push(C.byref(rb[m]), int(adc[s, t, m]))
+            if not all(r.is_full for r in rb):
+                continue
+            po = sum(R.rolling_buffer_get_outgoing_power(C.byref(r)) for r in rb)
+            pi = sum(R.rolling_buffer_get_incoming_power(C.byref(r)) for r in rb)
+            if po > thr + pi:
+                fr = []
+                for r in rb:
+                    b = O.RefBuffer()
+                    R.rolling_buffer_write_out(C.byref(r), C.byref(b))
+                    R.buffer_normalize_range(C.byref(b))
+                    R.buffer_window(C.byref(b))
+                    fr.append(np.frombuffer(bytes(b.buffer), np.int16).copy())
+                ends.append((s, t + 1))
+                frames.append(np.stack(fr))
+                for r in rb:
+                    R.rolling_buffer_init(C.byref(r))
+    res = O.stream_run(adc, N, fs, S_lag, win1024, lut, max_trig=32)
+    np.savez_compressed(os.path.join(OUT, "stream_trace.npz"), adc=adc, lut=lut, fs=fs,
+                        max_shift=S_lag, ref_ends=np.array(ends, np.int64),
+                        ref_prepared=np.array(frames, np.int16),
+                        **{"orc_" + k: v for k, v in res.items()})
+    print("stream trace:", len(ends), "reference triggers")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     O.build()
+    if sys.argv[1:] == ["stream"]:
+        tabs = dict(np.load(os.path.join(OUT, "window_q15.npz")))
+        mics = np.load(os.path.join(OUT, "ref_components.npz"))["mics"]
+        stream_fixture(tabs["n1024"], mics)
+        return
     tabs, pins = windows_fixture()
     print("window pins:", {k: v for k, v in pins.items() if "equals" in k})
     mics = ref_components_fixture(tabs["n1024"])
     pipeline_fixture(tabs["n1024"], mics)
     ema_fixture()
+    stream_fixture(tabs["n1024"], mics)
     print("fixtures written to", OUT)
 
 
