@@ -208,6 +208,12 @@ struct tdoa_ctx {
     // for weighted scores ([B][P][K] int64 or float); grows on demand
     void *d_wscratch = nullptr;
     size_t wscratch_bytes = 0;
+    // raw-score and cell scratch for the least-squares refinement
+    void *d_rscratch = nullptr;
+    size_t rscratch_bytes = 0;
+    void *d_cscratch = nullptr;
+    size_t cscratch_bytes = 0;
+    float *d_mic = nullptr;  // [M][2]
     // GCC_PHAT spectrum scratch for the two-pass shapes (M > 3 or N > 2048):
     // a fixed chunk of frames' spectra that stays in L2 / MALL between passes
     void *d_spec = nullptr;
@@ -300,6 +306,12 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_tuple_cell);
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_wscratch);
+    (void)hipFree(c->d_rscratch);
+    (void)hipFree(c->d_cscratch);
+    (void)hipFree(c->d_mic);
+    c->d_rscratch = c->d_cscratch = nullptr;
+    c->rscratch_bytes = c->cscratch_bytes = 0;
+    c->d_mic = nullptr;
     (void)hipFree(c->d_spec);
     c->d_spec = nullptr;
     c->spec_bytes = 0;
@@ -461,12 +473,15 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     if (hipMalloc(&c->d_window, sizeof(int16_t) * N) != hipSuccess ||
         hipMalloc(&c->d_prior, sizeof(float) * c->K) != hipSuccess ||
         hipMalloc(&c->d_tuples, sizeof(uint32_t) * c->tuples.size()) != hipSuccess ||
-        hipMalloc(&c->d_tuple_cell, sizeof(int32_t) * c->U) != hipSuccess) {
+        hipMalloc(&c->d_tuple_cell, sizeof(int32_t) * c->U) != hipSuccess ||
+        hipMalloc(&c->d_mic, sizeof(float) * 2 * M) != hipSuccess) {
         free_device(c);
         delete c;
         return fail(TDOA_ERR_NOMEM, "hipMalloc of context tables failed");
     }
     hipError_t e = hipMemcpy(c->d_window, w16.data(), sizeof(int16_t) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_mic, c->mic.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(c->d_prior, c->prior.data(), sizeof(float) * c->K, hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -514,6 +529,10 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     }
     kp.window = c->d_window;
     kp.prior = c->d_prior;
+    kp.mic_xy = c->d_mic;
+    kp.fs = (float)cfg->sample_rate_hz;
+    kp.c = cfg->speed_of_sound;
+    kp.height = cfg->height_offset;
     kp.tuples = c->d_tuples;
     kp.tuple_cell = c->d_tuple_cell;
     *out = c;
@@ -564,6 +583,21 @@ static tdoa_kout to_kout(const tdoa_outputs *o)
     return k;
 }
 
+// device scratch that grows on demand (synchronises the stream before a resize)
+static int grow(void **p, size_t *have, size_t need, void *stream, const char *what)
+{
+    if (need <= *have)
+        return TDOA_OK;
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipMalloc(p, need) != hipSuccess)
+        return fail(TDOA_ERR_NOMEM, "%s scratch of %zu bytes", what, need);
+    *have = need;
+    return TDOA_OK;
+}
+
 static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,
                      void *stream, bool prepared)
 {
@@ -580,32 +614,49 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     HIP_TRY(hipSetDevice(ctx->device));
     const bool phat = ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT && !prepared;
     tdoa_kout k = to_kout(out);
-    const bool grid = out->cell || out->xy || (phat ? out->max_Lf != nullptr : out->max_L != nullptr);
+    const bool ls = out->xy_ls || out->ls_rms;
+    const bool grid =
+        ls || out->cell || out->xy || (phat ? out->max_Lf != nullptr : out->max_L != nullptr);
+    const size_t sz = phat ? sizeof(float) : sizeof(int64_t);
+    const size_t pk = (size_t)B * ctx->P * ctx->K * sz;
     const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
     if (grid && !weighted) {
         // the grid kernel reads the weighted scores back: keep them in scratch
-        const size_t need = (size_t)B * ctx->P * ctx->K * (phat ? sizeof(float) : sizeof(int64_t));
-        if (need > ctx->wscratch_bytes) {
-            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-            (void)hipFree(ctx->d_wscratch);
-            ctx->d_wscratch = nullptr;
-            ctx->wscratch_bytes = 0;
-            if (hipMalloc(&ctx->d_wscratch, need) != hipSuccess)
-                return fail(TDOA_ERR_NOMEM, "weighted-score scratch of %zu bytes", need);
-            ctx->wscratch_bytes = need;
-        }
+        int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, pk, stream, "weighted-score");
+        if (rc)
+            return rc;
         weighted = ctx->d_wscratch;
         if (phat)
             k.weighted_f = (float *)ctx->d_wscratch;
         else
             k.weighted = (int64_t *)ctx->d_wscratch;
     }
+    const void *raw = phat ? (const void *)out->scores_f : (const void *)out->scores;
+    if (ls && !raw) {  // the refinement reads the raw scores around each peak
+        int rc = grow(&ctx->d_rscratch, &ctx->rscratch_bytes, pk, stream, "raw-score");
+        if (rc)
+            return rc;
+        raw = ctx->d_rscratch;
+        if (phat)
+            k.scores_f = (float *)ctx->d_rscratch;
+        else
+            k.scores = (int64_t *)ctx->d_rscratch;
+    }
+    if (ls && !out->cell) {
+        int rc = grow(&ctx->d_cscratch, &ctx->cscratch_bytes, (size_t)B * 4, stream, "cell");
+        if (rc)
+            return rc;
+        k.cell = (int32_t *)ctx->d_cscratch;
+    }
     int rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, ctx->d_spec,
                                          ctx->spec_bytes, stream)
                   : tdoa_launch_direct(ctx->kp, k, frames, B, prepared, stream, nullptr);
     if (rc != 0 || !grid)
         return rc;
-    return tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
+    rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
+    if (rc != 0 || !ls)
+        return rc;
+    return tdoa_launch_ls(ctx->kp, raw, phat, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);
 }
 
 // accessors for the streaming pipeline (tdoa_stream.cpp)

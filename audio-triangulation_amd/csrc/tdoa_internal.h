@@ -6,6 +6,8 @@
 #include <stdint.h>
 
 #define TDOA_MAX_PAIRS 28  // 8 mics
+#define TDOA_MAX_MICS_K 8
+#define TDOA_LS_ITERS 10   // least-squares refinement steps (tdoa_ls.hip)
 
 // Lag tiling of the DIRECT kernel: each work item owns TDOA_LT consecutive
 // lags (an even start lag, so even lags read word-aligned sample pairs and odd
@@ -39,6 +41,9 @@ struct tdoa_kparams {
     const int32_t *tuple_cell; // [U] first row-major cell of each tuple
     const float *tw;           // GCC_PHAT: e^{-2 pi i k/N}, k < N   (re, im)
     const float *tw2;          // GCC_PHAT: e^{-2 pi i k/2N}, k <= N (re, im)
+    // least-squares refinement (tdoa_ls.hip)
+    const float *mic_xy;       // [M][2] metres
+    float fs, c, height;
 };
 
 struct tdoa_kout {
@@ -91,6 +96,9 @@ int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
                        const int16_t *frames, int64_t B, bool prepared,
                        void *stream, int *lds_bytes_out,
                        const int32_t *count_dev = nullptr);
+int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
+                   const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
+                   int64_t B, void *stream);
 size_t tdoa_stream_trigger_lds(int M, int N, int H);
 int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream);
 int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &kp,

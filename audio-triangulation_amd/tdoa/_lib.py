@@ -62,7 +62,7 @@ class Outputs(C.Structure):
     """struct tdoa_outputs (include/tdoa.h): device pointers."""
     _fields_ = [(n, C.c_void_p) for n in (
         "lags", "gate", "cell", "xy", "max_L", "max_Lf", "scores", "weighted",
-        "scores_f", "weighted_f")]
+        "scores_f", "weighted_f", "xy_ls", "ls_rms")]
 
 
 class StreamOutputs(C.Structure):

@@ -119,7 +119,8 @@ class Localizer:
         return p
 
     # ---------------------------------------------------------- compute
-    def alloc_outputs(self, B: int, scores: bool = False, grid: bool = True) -> dict:
+    def alloc_outputs(self, B: int, scores: bool = False, grid: bool = True,
+                      ls: bool = False) -> dict:
         dev, P, K = self.torch_device, self.dims.P, self.dims.K
         o = {"lags": torch.empty((B, P), dtype=torch.int32, device=dev),
              "gate": torch.empty(B, dtype=torch.uint8, device=dev)}
@@ -130,6 +131,9 @@ class Localizer:
                 o["max_L"] = torch.empty(B, dtype=torch.int64, device=dev)
             else:
                 o["max_Lf"] = torch.empty(B, dtype=torch.float32, device=dev)
+        if ls:
+            o["xy_ls"] = torch.empty((B, 2), dtype=torch.float32, device=dev)
+            o["ls_rms"] = torch.empty(B, dtype=torch.float32, device=dev)
         if scores:
             if self.engine == "direct":
                 o["scores"] = torch.empty((B, P, K), dtype=torch.int64, device=dev)
@@ -168,8 +172,8 @@ class Localizer:
         return out
 
     def localize(self, frames: torch.Tensor, scores: bool = False, grid: bool = True,
-                 stream=None) -> dict:
-        out = self.alloc_outputs(self._check_frames(frames), scores=scores, grid=grid)
+                 stream=None, ls: bool = False) -> dict:
+        out = self.alloc_outputs(self._check_frames(frames), scores=scores, grid=grid, ls=ls)
         return self.localize_into(frames, out, stream)
 
     def correlate_prepared(self, prepared: torch.Tensor, scores: bool = True,

@@ -93,6 +93,12 @@ typedef struct tdoa_outputs {
     int64_t *weighted;       /* [B][P][K] DIRECT scores after the lag prior  */
     float *scores_f;         /* [B][P][K] GCC_PHAT raw correlation (debug)   */
     float *weighted_f;       /* [B][P][K] GCC_PHAT after the lag prior       */
+    /* Least-squares refinement of the grid argmax (extension; absent in the
+     * reference): sub-sample lags (parabolic vertex of the raw scores) fitted
+     * by 10 Levenberg-Marquardt steps in double precision on the LUT's
+     * hemisphere geometry, starting at the argmax cell, clamped to the grid. */
+    float *xy_ls;            /* [B][2] refined (x, y) metres, grid frame     */
+    float *ls_rms;           /* [B] rms lag residual (samples)               */
 } tdoa_outputs;
 
 typedef struct tdoa_ctx tdoa_ctx;

@@ -58,6 +58,9 @@ def lib():
         L.orc_stream_run.argtypes = [P, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                      C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P]
         L.orc_stream_run.restype = C.c_int
+        L.orc_ls_refine.argtypes = [P, P, C.c_int, C.c_int, P, C.c_int32, C.c_int, C.c_int,
+                                    C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
+                                    P, P, P]
         _lib = L
     return _lib
 
@@ -109,6 +112,26 @@ def stream_run(adc: np.ndarray, N: int, fs: int, max_shift: int, win: np.ndarray
     if rc != 0:
         raise ValueError("orc_stream_run rejected the shape")
     return r
+
+
+def ls_refine(scores, best, mic_xy, cell, half_w=50, half_h=50, grid_scale=24.0,
+              height=1.2, fs=50000.0, c=343.0, iters=10):
+    """a15 least squares for B frames: scores [B][P][K] raw (any numeric dtype),
+    best [B][P], cell [B] -> (uv [B][2] float64, rms [B])."""
+    sc = np.ascontiguousarray(scores, dtype=np.float64)
+    B, P, K = sc.shape
+    M = int(round((1 + np.sqrt(1 + 8 * P)) / 2))
+    bst = np.ascontiguousarray(best, dtype=np.int32)
+    mic = np.ascontiguousarray(mic_xy, dtype=np.float32).reshape(-1)
+    uv = np.zeros((B, 2), np.float64)
+    rms = np.zeros(B, np.float64)
+    u, v, r = C.c_double(), C.c_double(), C.c_double()
+    for f in range(B):
+        lib().orc_ls_refine(_p(sc[f]), _p(bst[f]), M, K, _p(mic), int(cell[f]), half_w, half_h,
+                            grid_scale, height, fs, c, iters, C.byref(u), C.byref(v), C.byref(r))
+        uv[f] = (u.value, v.value)
+        rms[f] = r.value
+    return uv, rms
 
 
 # ---------------------------------------------------------------- stages

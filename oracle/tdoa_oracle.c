@@ -445,3 +445,76 @@ int orc_stream_run(const uint8_t *adc, int64_t S, int64_t T, int M, int N, int f
     }
     return 0;
 }
+
+/* a15: see tdoa_oracle.h.  Sub-sample lag of pair p from its raw scores. */
+static double ls_tau(const double *s, int K, int best)
+{
+    const int S = K / 2, kb = best + S;
+    double d = 0.0;
+    if (kb > 0 && kb < K - 1) {
+        const double y0 = s[kb - 1], y1 = s[kb], y2 = s[kb + 1];
+        const double den = y0 - 2.0 * y1 + y2;
+        if (den < 0.0) {
+            d = 0.5 * (y0 - y2) / den;
+            d = d < -0.5 ? -0.5 : (d > 0.5 ? 0.5 : d);
+        }
+    }
+    return (double)best + d;
+}
+
+void orc_ls_refine(const double *scores, const int32_t *best, int M, int K,
+                   const float *mic_xy, int32_t cell, int half_w, int half_h,
+                   double grid_scale, double height, double fs, double c, int iters,
+                   double *u_out, double *v_out, double *rms_out)
+{
+    const int P = M * (M - 1) / 2, W = 2 * half_w + 1;
+    double tau[64 * 63 / 2];
+    for (int p = 0; p < P; p++)
+        tau[p] = ls_tau(scores + (size_t)p * K, K, best[p]);
+    double u = (double)(cell % W - half_w) / grid_scale;
+    double v = (double)(half_h - cell / W) / grid_scale;
+    const double lu = (double)half_w / grid_scale, lv = (double)half_h / grid_scale;
+    const double h = height, kf = fs / c;
+    double ss = 0.0;
+    for (int it = 0; it <= iters; it++) {
+        /* point on the hemisphere and its derivatives */
+        const double n2 = u * u + v * v + h * h, n = sqrt(n2), n3 = n2 * n;
+        const double k = h / n;
+        const double px = k * u, py = k * v, pz = k * h;
+        const double dxu = h * (1.0 / n - u * u / n3), dyu = h * (-v * u / n3), dzu = h * (-h * u / n3);
+        const double dxv = h * (-u * v / n3), dyv = h * (1.0 / n - v * v / n3), dzv = h * (-h * v / n3);
+        double d[64], du[64], dv[64];
+        for (int m = 0; m < M; m++) {
+            const double ex = px - (double)mic_xy[2 * m], ey = py - (double)mic_xy[2 * m + 1], ez = pz;
+            d[m] = sqrt(ex * ex + ey * ey + ez * ez);
+            du[m] = (ex * dxu + ey * dyu + ez * dzu) / d[m];
+            dv[m] = (ex * dxv + ey * dyv + ez * dzv) / d[m];
+        }
+        double a11 = 0.0, a12 = 0.0, a22 = 0.0, g1 = 0.0, g2 = 0.0;
+        ss = 0.0;
+        int p = 0;
+        for (int i = 0; i < M; i++)
+            for (int j = i + 1; j < M; j++, p++) {
+                const double r = (d[j] - d[i]) * kf - tau[p];
+                const double ju = (du[j] - du[i]) * kf, jv = (dv[j] - dv[i]) * kf;
+                a11 += ju * ju;
+                a12 += ju * jv;
+                a22 += jv * jv;
+                g1 += ju * r;
+                g2 += jv * r;
+                ss += r * r;
+            }
+        if (it == iters)
+            break;
+        const double lam = 1e-3 * (a11 + a22) + 1e-12;
+        const double b11 = a11 + lam, b22 = a22 + lam;
+        const double det = b11 * b22 - a12 * a12;
+        u -= (b22 * g1 - a12 * g2) / det;
+        v -= (b11 * g2 - a12 * g1) / det;
+        u = u < -lu ? -lu : (u > lu ? lu : u);
+        v = v < -lv ? -lv : (v > lv ? lv : v);
+    }
+    *u_out = u;
+    *v_out = v;
+    *rms_out = sqrt(ss / (double)P);
+}

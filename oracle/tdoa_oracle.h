@@ -128,6 +128,20 @@ int orc_stream_run(const uint8_t *adc /* [S][T][M] */, int64_t S, int64_t T, int
                    const uint8_t *lut, int half_w, int half_h, int max_trig,
                    int threads, orc_stream_out *out);
 
+/* ---- a15 (north-star extension, absent in the reference): least-squares
+ *      refinement of the grid argmax from sub-sample lags, double precision.
+ *      tau_p = best_p + parabolic vertex of the raw scores at best-1..best+1
+ *      (0 at the lag-window edges or a non-concave triple, clamped to
+ *      +-0.5); model pred_p(u, v) = (d_j - d_i) fs / c with the LUT's
+ *      geometry (grid metres (u, v), hemisphere projection of radius h,
+ *      vga_heatmap.h:55-65); `iters` Levenberg-Marquardt steps
+ *      (lambda = 1e-3 trace(J'J) + 1e-12) from the argmax cell's (u, v),
+ *      clamped to the grid.  Outputs (u, v) and the rms lag residual. ---- */
+void orc_ls_refine(const double *scores /* [P][K] raw */, const int32_t *best /* [P] */,
+                   int M, int K, const float *mic_xy, int32_t cell, int half_w,
+                   int half_h, double grid_scale, double height, double fs, double c,
+                   int iters, double *u, double *v, double *rms);
+
 #ifdef __cplusplus
 }
 #endif
