@@ -214,6 +214,7 @@ struct tdoa_ctx {
     void *d_cscratch = nullptr;
     size_t cscratch_bytes = 0;
     float *d_mic = nullptr;  // [M][2]
+    uint8_t *d_lut = nullptr;  // [P][G]
     // GCC_PHAT spectrum scratch for the two-pass shapes (M > 3 or N > 2048):
     // a fixed chunk of frames' spectra that stays in L2 / MALL between passes
     void *d_spec = nullptr;
@@ -309,6 +310,8 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_rscratch);
     (void)hipFree(c->d_cscratch);
     (void)hipFree(c->d_mic);
+    (void)hipFree(c->d_lut);
+    c->d_lut = nullptr;
     c->d_rscratch = c->d_cscratch = nullptr;
     c->rscratch_bytes = c->cscratch_bytes = 0;
     c->d_mic = nullptr;
@@ -474,7 +477,8 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         hipMalloc(&c->d_prior, sizeof(float) * c->K) != hipSuccess ||
         hipMalloc(&c->d_tuples, sizeof(uint32_t) * c->tuples.size()) != hipSuccess ||
         hipMalloc(&c->d_tuple_cell, sizeof(int32_t) * c->U) != hipSuccess ||
-        hipMalloc(&c->d_mic, sizeof(float) * 2 * M) != hipSuccess) {
+        hipMalloc(&c->d_mic, sizeof(float) * 2 * M) != hipSuccess ||
+        hipMalloc(&c->d_lut, c->lut.size()) != hipSuccess) {
         free_device(c);
         delete c;
         return fail(TDOA_ERR_NOMEM, "hipMalloc of context tables failed");
@@ -482,6 +486,8 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     hipError_t e = hipMemcpy(c->d_window, w16.data(), sizeof(int16_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(c->d_mic, c->mic.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(c->d_lut, c->lut.data(), c->lut.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(c->d_prior, c->prior.data(), sizeof(float) * c->K, hipMemcpyHostToDevice);
     if (e == hipSuccess)
@@ -530,6 +536,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     kp.window = c->d_window;
     kp.prior = c->d_prior;
     kp.mic_xy = c->d_mic;
+    kp.lut = c->d_lut;
     kp.fs = (float)cfg->sample_rate_hz;
     kp.c = cfg->speed_of_sound;
     kp.height = cfg->height_offset;
@@ -657,6 +664,17 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     if (rc != 0 || !ls)
         return rc;
     return tdoa_launch_ls(ctx->kp, raw, phat, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);
+}
+
+extern "C" int tdoa_heatmap(tdoa_ctx *ctx, const void *weighted, const void *max_L, int is_float,
+                            int64_t B, uint8_t *classes, void *stream)
+{
+    if (!ctx || !weighted || !max_L || !classes)
+        return fail(TDOA_ERR_INVALID, "tdoa_heatmap: NULL argument");
+    if (B < 0)
+        return fail(TDOA_ERR_INVALID, "tdoa_heatmap: negative batch");
+    HIP_TRY(hipSetDevice(ctx->device));
+    return tdoa_launch_heatmap(ctx->kp, weighted, max_L, is_float != 0, B, classes, stream);
 }
 
 // accessors for the streaming pipeline (tdoa_stream.cpp)

@@ -212,7 +212,56 @@ int launch(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int6
     return e == hipSuccess ? 0 : hip_fail(e, "k_grid launch");
 }
 
+// vga_heatmap.h:110-130 colouring pass as classes: 4 white (L >= 63/64 max),
+// 3 green (31/32), 2 red (15/16), 1 blue (7/8), 0 black; thresholds are the
+// reference's int64 (max * n) >> b; for float scores max * n / 2^b.
+__device__ __forceinline__ int64_t thr_t(int64_t mx, int n, int b) { return (mx * n) >> b; }
+__device__ __forceinline__ float thr_t(float mx, int n, int b) { return mx * ((float)n / (float)(1 << b)); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_heatmap(tdoa_kparams kp, const T *__restrict__ weighted,
+                                                 const T *__restrict__ max_L,
+                                                 uint8_t *__restrict__ classes)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T *W = (T *)smem;  // [P][K]
+    const int64_t f = blockIdx.y;
+    const int P = kp.P, K = kp.K, G = kp.G, tid = threadIdx.x;
+    for (int e = tid; e < P * K; e += blockDim.x)
+        W[e] = weighted[(size_t)f * P * K + e];
+    __syncthreads();
+    const T mx = max_L[f];
+    const T tw = thr_t(mx, 63, 6), tg = thr_t(mx, 31, 5), tr = thr_t(mx, 15, 4), tb = thr_t(mx, 7, 3);
+    const int c = blockIdx.x * blockDim.x + tid;
+    if (c >= G)
+        return;
+    T L = 0;
+    for (int p = 0; p < P; p++)
+        L += W[p * K + kp.lut[(size_t)p * G + c]];
+    classes[(size_t)f * G + c] = L >= tw ? 4 : L >= tg ? 3 : L >= tr ? 2 : L >= tb ? 1 : 0;
+}
+
 }  // namespace
+
+int tdoa_launch_heatmap(const tdoa_kparams &kp, const void *weighted, const void *max_L,
+                        bool is_float, int64_t B, uint8_t *classes, void *stream)
+{
+    if (B <= 0)
+        return 0;
+    if (B > 65535)
+        return tdoa_set_error(-1, "heatmap: at most 65535 frames per call");
+    const dim3 grid((unsigned)((kp.G + 255) / 256), (unsigned)B);
+    const size_t lds = (size_t)kp.P * kp.K * (is_float ? 4 : 8);
+    hipStream_t st = (hipStream_t)stream;
+    if (is_float)
+        hipLaunchKernelGGL(k_heatmap<float>, grid, dim3(256), lds, st, kp, (const float *)weighted,
+                           (const float *)max_L, classes);
+    else
+        hipLaunchKernelGGL(k_heatmap<int64_t>, grid, dim3(256), lds, st, kp,
+                           (const int64_t *)weighted, (const int64_t *)max_L, classes);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "k_heatmap launch");
+}
 
 int tdoa_launch_grid(const tdoa_kparams &kp, const tdoa_kout &out, const void *weighted,
                      bool is_float, int64_t B, void *stream)

@@ -41,6 +41,7 @@ struct tdoa_kparams {
     const int32_t *tuple_cell; // [U] first row-major cell of each tuple
     const float *tw;           // GCC_PHAT: e^{-2 pi i k/N}, k < N   (re, im)
     const float *tw2;          // GCC_PHAT: e^{-2 pi i k/2N}, k <= N (re, im)
+    const uint8_t *lut;        // [P][G] lag index per cell (heat map)
     // least-squares refinement (tdoa_ls.hip)
     const float *mic_xy;       // [M][2] metres
     float fs, c, height;
@@ -96,6 +97,8 @@ int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
                        const int16_t *frames, int64_t B, bool prepared,
                        void *stream, int *lds_bytes_out,
                        const int32_t *count_dev = nullptr);
+int tdoa_launch_heatmap(const tdoa_kparams &kp, const void *weighted, const void *max_L,
+                        bool is_float, int64_t B, uint8_t *classes, void *stream);
 int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
                    const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
                    int64_t B, void *stream);

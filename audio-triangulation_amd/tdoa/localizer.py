@@ -203,6 +203,19 @@ class Localizer:
                                         _ptr(best), sol, C.c_void_p(st.cuda_stream)),
               "tdoa_average_batch")
 
+    def heatmap(self, weighted: torch.Tensor, max_L: torch.Tensor) -> torch.Tensor:
+        """vga_heatmap.h:110-130 colour classes [B][H][W] (4 white .. 0 black)."""
+        B = weighted.shape[0]
+        is_float = weighted.dtype == torch.float32
+        assert weighted.dtype in (torch.int64, torch.float32) and max_L.dtype == weighted.dtype
+        assert tuple(weighted.shape[1:]) == (self.dims.P, self.dims.K) and weighted.is_contiguous()
+        H = self.dims.G // self.grid_W
+        out = torch.empty((B, H, self.grid_W), dtype=torch.uint8, device=self.torch_device)
+        st = torch.cuda.current_stream(self.torch_device)
+        check(load().tdoa_heatmap(self._ctx, _ptr(weighted), _ptr(max_L), int(is_float), B,
+                                  _ptr(out), C.c_void_p(st.cuda_stream)), "tdoa_heatmap")
+        return out
+
     def cell_xy(self, cell: np.ndarray) -> np.ndarray:
         """((x - half_w)/scale, (half_h - y)/scale) of row-major cells, float32 as on device."""
         cell = np.asarray(cell)

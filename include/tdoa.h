@@ -135,6 +135,16 @@ int tdoa_average_batch(tdoa_ctx *ctx, int64_t S, int64_t *est,
                        const int64_t *fresh, const float *decay, int32_t *best,
                        const tdoa_outputs *solve, void *stream);
 
+/* Heat-map classes of vga_draw_heatmap's colouring pass (vga_heatmap.h:
+ * 110-130) for B frames: classes[B][G] = 4 (white, L >= (max*63)>>6),
+ * 3 (green, (max*31)>>5), 2 (red, (max*15)>>4), 1 (blue, (max*7)>>3), else 0,
+ * L = sum_p weighted_p[LUT_p].  weighted [B][P][K] and max_L [B] are device
+ * int64 (is_float = 0; the reference's integer thresholds) or float
+ * (is_float = 1; max * n / 2^b), e.g. a localize call's weighted / max_L
+ * outputs or EMA scores with their grid max.  B <= 65535. */
+int tdoa_heatmap(tdoa_ctx *ctx, const void *weighted, const void *max_L, int is_float,
+                 int64_t B, uint8_t *classes, void *stream);
+
 /* Host helper: decay of correlations.c:42-43 from integer-us timestamps. */
 float tdoa_decay_us(uint64_t now_us, uint64_t last_us);
 

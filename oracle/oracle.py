@@ -58,6 +58,7 @@ def lib():
         L.orc_stream_run.argtypes = [P, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                      C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P]
         L.orc_stream_run.restype = C.c_int
+        L.orc_heatmap.argtypes = [P, C.c_int, C.c_int, P, C.c_int, P]
         L.orc_ls_refine.argtypes = [P, P, C.c_int, C.c_int, P, C.c_int32, C.c_int, C.c_int,
                                     C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
                                     P, P, P]
@@ -112,6 +113,16 @@ def stream_run(adc: np.ndarray, N: int, fs: int, max_shift: int, win: np.ndarray
     if rc != 0:
         raise ValueError("orc_stream_run rejected the shape")
     return r
+
+
+def heatmap(weighted: np.ndarray, lut: np.ndarray) -> np.ndarray:
+    """vga_heatmap.h:97-130 classes for one frame: weighted int64 [P][K], lut [P][G]."""
+    w = np.ascontiguousarray(weighted, dtype=np.int64)
+    P, K = w.shape
+    lt = np.ascontiguousarray(lut, dtype=np.uint8).reshape(P, -1)
+    out = np.zeros(lt.shape[1], np.uint8)
+    lib().orc_heatmap(_p(w), P, K, _p(lt), lt.shape[1], _p(out))
+    return out
 
 
 def ls_refine(scores, best, mic_xy, cell, half_w=50, half_h=50, grid_scale=24.0,

@@ -518,3 +518,27 @@ void orc_ls_refine(const double *scores, const int32_t *best, int M, int K,
     *v_out = v;
     *rms_out = sqrt(ss / (double)P);
 }
+
+/* vga_heatmap.h:97-130: max pass, thresholds (max*63)>>6, (max*31)>>5,
+ * (max*15)>>4, (max*7)>>3 (int64, arithmetic shifts), then the class of
+ * every cell. */
+void orc_heatmap(const int64_t *weighted, int P, int K, const uint8_t *lut, int G,
+                 uint8_t *classes)
+{
+    int64_t hi = INT64_MIN;
+    for (int c = 0; c < G; c++) {
+        int64_t L = 0;
+        for (int p = 0; p < P; p++)
+            L += weighted[(size_t)p * K + lut[(size_t)p * G + c]];
+        if (L > hi)
+            hi = L;
+    }
+    const int64_t tw = asr64(hi * 63, 6), tg = asr64(hi * 31, 5), tr = asr64(hi * 15, 4),
+                  tb = asr64(hi * 7, 3);
+    for (int c = 0; c < G; c++) {
+        int64_t L = 0;
+        for (int p = 0; p < P; p++)
+            L += weighted[(size_t)p * K + lut[(size_t)p * G + c]];
+        classes[c] = L >= tw ? 4 : L >= tg ? 3 : L >= tr ? 2 : L >= tb ? 1 : 0;
+    }
+}

@@ -128,6 +128,11 @@ int orc_stream_run(const uint8_t *adc /* [S][T][M] */, int64_t S, int64_t T, int
                    const uint8_t *lut, int half_w, int half_h, int max_trig,
                    int threads, orc_stream_out *out);
 
+/* ---- f4: vga_heatmap.h:110-130 colouring as classes 4..0 (white, green,
+ *      red, blue, black) with the reference's int64 thresholds. ---- */
+void orc_heatmap(const int64_t *weighted /* [P][K] */, int P, int K, const uint8_t *lut,
+                 int G, uint8_t *classes /* [G] */);
+
 /* ---- a15 (north-star extension, absent in the reference): least-squares
  *      refinement of the grid argmax from sub-sample lags, double precision.
  *      tau_p = best_p + parabolic vertex of the raw scores at best-1..best+1
