@@ -627,7 +627,8 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     const size_t sz = phat ? sizeof(float) : sizeof(int64_t);
     const size_t pk = (size_t)B * ctx->P * ctx->K * sz;
     const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
-    if (grid && !weighted) {
+    const bool fused_grid = phat && tdoa_gcc_phat_fused_grid(ctx->kp);
+    if (grid && !weighted && !fused_grid) {
         // the grid kernel reads the weighted scores back: keep them in scratch
         int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, pk, stream, "weighted-score");
         if (rc)
@@ -660,7 +661,8 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
                   : tdoa_launch_direct(ctx->kp, k, frames, B, prepared, stream, nullptr);
     if (rc != 0 || !grid)
         return rc;
-    rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
+    if (!fused_grid)
+        rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
     if (rc != 0 || !ls)
         return rc;
     return tdoa_launch_ls(ctx->kp, raw, phat, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);

@@ -357,6 +357,121 @@ __device__ __forceinline__ int swz(int row, int col)
 
 __device__ __forceinline__ f2 ldf2(const float *p, int k) { return f2{p[2 * k], p[2 * k + 1]}; }
 
+// Grid solve (vga_heatmap.h:99-108 on float scores) for the ns frames whose
+// weighted scores sit in wsc[p][k][slot]: every lane scores its tuples for all
+// GSLOTS slots at once (two b128 LDS reads per pair), strict '>' over
+// increasing tuples per lane, then (max, first tuple) across the workgroup.
+constexpr int GSLOTS = 8;
+
+// (max value, first index) combine through one DPP lane move (no LDS round
+// trip).  Lanes whose row is outside ROWMASK keep their own value (old = src).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_argmax(float &v, int &i)
+{
+    const int vb = __builtin_bit_cast(int, v);
+    const float ov =
+        __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(vb, vb, CTRL, ROWMASK, 0xF, false));
+    const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWMASK, 0xF, false);
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+// within each 16-lane row: xor 1, xor 2 (quad_perm), half-row mirror, row mirror
+__device__ __forceinline__ void row_argmax(float &v, int &i)
+{
+    dpp_argmax<0xB1, 0xF>(v, i);
+    dpp_argmax<0x4E, 0xF>(v, i);
+    dpp_argmax<0x141, 0xF>(v, i);
+    dpp_argmax<0x140, 0xF>(v, i);
+}
+// whole wave -> lane 63 (row_bcast:15 into rows 1, 3; row_bcast:31 into rows 2, 3)
+__device__ __forceinline__ void wave_argmax_to63(float &v, int &i)
+{
+    row_argmax(v, i);
+    dpp_argmax<0x142, 0xA>(v, i);
+    dpp_argmax<0x143, 0xC>(v, i);
+}
+// each 32-lane half-wave -> its lane 31 / 63
+__device__ __forceinline__ void half_argmax_to31(float &v, int &i)
+{
+    row_argmax(v, i);
+    dpp_argmax<0x142, 0xA>(v, i);
+}
+__device__ __forceinline__ void grid_tail(const tdoa_kparams &kp, const tdoa_kout &out,
+                                          const float *wsc, const int64_t *gfr, float *gredv,
+                                          int *gredi, int ns, uint32_t *tups)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, K = kp.K;
+    // stage the tuple table (U words) in the idle FFT buffers: all loads in flight together
+#pragma unroll 8
+    for (int e = tid; e < kp.U; e += 192)
+        tups[e] = kp.tuples[e];
+    __syncthreads();
+    float bv[GSLOTS];
+    int bu[GSLOTS];
+#pragma unroll
+    for (int f = 0; f < GSLOTS; f++) {
+        bv[f] = -INFINITY;
+        bu[f] = INT_MAX;
+    }
+    for (int u = tid; u < kp.U; u += 192) {
+        const uint32_t word = tups[u];
+        float L[GSLOTS];
+#pragma unroll
+        for (int f = 0; f < GSLOTS; f++)
+            L[f] = 0.0f;
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+            const float4 *src = reinterpret_cast<const float4 *>(
+                wsc + (p * K + (int)((word >> (8 * p)) & 0xFFu)) * GSLOTS);
+            const float4 a = src[0], b = src[1];
+            L[0] += a.x;
+            L[1] += a.y;
+            L[2] += a.z;
+            L[3] += a.w;
+            L[4] += b.x;
+            L[5] += b.y;
+            L[6] += b.z;
+            L[7] += b.w;
+        }
+#pragma unroll
+        for (int f = 0; f < GSLOTS; f++)
+            if (L[f] > bv[f]) {
+                bv[f] = L[f];
+                bu[f] = u;
+            }
+    }
+#pragma unroll
+    for (int f = 0; f < GSLOTS; f++) {
+        wave_argmax_to63(bv[f], bu[f]);
+        if (lane == 63) {
+            gredv[wave * GSLOTS + f] = bv[f];
+            gredi[wave * GSLOTS + f] = bu[f];
+        }
+    }
+    __syncthreads();
+    if (tid < ns) {
+        float v = gredv[tid];
+        int ui = gredi[tid];
+        for (int w = 1; w < 3; w++)
+            better(v, ui, gredv[w * GSLOTS + tid], gredi[w * GSLOTS + tid]);
+        if (ui < 0 || ui >= kp.U)  // every L compared false (NaN scores)
+            ui = 0;
+        const int cell = kp.tuple_cell[ui];
+        const int64_t fi = gfr[tid];
+        if (out.cell)
+            out.cell[fi] = cell;
+        if (out.max_Lf)
+            out.max_Lf[fi] = v;
+        if (out.xy) {
+            const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+            out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
+            out.xy[2 * fi + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_kout out,
                                                           const int16_t *__restrict__ frames,
                                                           int64_t B, float eps2)
@@ -369,6 +484,13 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
     f2 *tw2s = twm + 1024;                      // [513] W_2048^k, k <= N/2
     f2 *wins = tw2s + 514;                      // [512] Q15 window / 128, sample pairs
     int *bestlag = (int *)(wins + 512);         // [2][P]
+    // grid tail: weighted scores of the last GSLOTS frames, [p][k][slot], and
+    // their frame indices / reduction slots
+    float *wsc = (float *)(bestlag + 8);        // [P][K <= 127][GSLOTS]
+    int64_t *gfr = (int64_t *)(wsc + P * 128 * GSLOTS);  // [GSLOTS]
+    float *gredv = (float *)(gfr + GSLOTS);     // [3][GSLOTS]
+    int *gredi = (int *)(gredv + 3 * GSLOTS);   // [3][GSLOTS]
+    const bool do_grid = out.cell || out.xy || out.max_Lf;
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 31;
     const int h = wave * 2 + ((tid >> 5) & 1);  // half-wave: frame h/3, mic (then pair) h%3
@@ -410,6 +532,7 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
     unsigned long long ph_t = __builtin_amdgcn_s_memtime();
     int ph_it = 0;
 #endif
+    int nslot = 0;  // frames waiting in wsc for the grid tail
     for (int64_t pair = blockIdx.x; pair < npairs; pair += gridDim.x) {
 #ifdef TDOA_DIAG
         ph_it++;
@@ -573,10 +696,8 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
                     bv = cv[c];
                     bk = ck[c];
                 }
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1)
-                better(bv, bk, __shfl_xor(bv, o, 64), __shfl_xor(bk, o, 64));
-            bk = __shfl(bk, 0, 32);  // uniform per half-wave even for NaN scores
+            half_argmax_to31(bv, bk);
+            bk = __shfl(bk, 31, 32);  // uniform per half-wave even for NaN scores
             bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
             if (fr < nf) {
                 const size_t gb = (size_t)((f0 + fr) * P + mp) * K;
@@ -589,11 +710,15 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
                             out.scores_f[gb + ck[c]] = cv[c];
                         if (out.weighted_f)
                             out.weighted_f[gb + ck[c]] = wv;
+                        if (do_grid)
+                            wsc[(mp * K + ck[c]) * GSLOTS + nslot + fr] = wv;
                     }
                 }
                 if (lane == 0) {
                     bestlag[fr * P + mp] = bk - S;
                     out.lags[(f0 + fr) * P + mp] = bk - S;
+                    if (mp == 0)
+                        gfr[nslot + fr] = f0 + fr;
                 }
             }
         }
@@ -608,6 +733,12 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         }
         PH_MARK(3);
         __syncthreads();  // bestlag / buffers are rewritten by the next pair
+        nslot += nf;
+        if (do_grid && (nslot == GSLOTS || pair + gridDim.x >= npairs)) {
+            grid_tail(kp, out, wsc, gfr, gredv, gredi, nslot, (uint32_t *)bufs);
+            nslot = 0;
+            __syncthreads();  // wsc / reduction slots are rewritten next
+        }
         PH_MARK(4);
     }
 #ifdef TDOA_DIAG
@@ -620,6 +751,13 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
 }
 
 bool tdoa_gcc_phat_needs_split(int M, int N) { return M > 3 || N > 2048; }
+
+// the N = 1024, 3-mic kernel runs the grid solve itself (grid_tail)
+bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp)
+{
+    // the tuple table is staged in the 48 KiB of FFT buffers
+    return kp.M == 3 && kp.N == 1024 && kp.S <= 63 && kp.TW == 1 && kp.U <= 6 * 1024 * 2;
+}
 
 int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
                          int64_t B, float phat_eps, void *spec_scratch, size_t spec_bytes,
@@ -638,9 +776,11 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
                                           eps2 * 1152921504606846976.0f /* 2^60: int16 units */,
                                           spec_scratch, spec_bytes, stream);
     hipStream_t st = (hipStream_t)stream;
-    if (kp.M == 3 && kp.N == 1024 && kp.S <= 63) {
+    if (tdoa_gcc_phat_fused_grid(kp)) {
         // persistent 2-frame workgroups, as many as are resident at once
-        const size_t lds1024 = 7 * 1024 * 8 + 514 * 8 + 512 * 8 + 8 * 4;
+        // + grid tail: [3][128][8] scores, 8 frame indices, [3][8] reductions
+        const size_t lds1024 = 7 * 1024 * 8 + 514 * 8 + 512 * 8 + 8 * 4 + 3 * 128 * GSLOTS * 4 +
+                               GSLOTS * 8 + 3 * GSLOTS * 8;
         // resident workgroups for this LDS size (cached per device / size)
         static int c_dev = -1, c_resident = 0;
         static size_t c_lds = 0;

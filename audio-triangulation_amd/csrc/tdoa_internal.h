@@ -117,6 +117,7 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
 // GCC-PHAT shapes the fused kernels cannot hold (M > 3 or N > 2048): two
 // passes per chunk of frames through a spectrum scratch (tdoa_phat_split.hip)
 bool tdoa_gcc_phat_needs_split(int M, int N);
+bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
 int tdoa_launch_gcc_phat_split(const tdoa_kparams &kp, const tdoa_kout &out,
                                const int16_t *frames, int64_t B, float eps2_int16,
                                void *scratch, size_t scratch_bytes, void *stream);
