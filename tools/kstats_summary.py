@@ -11,6 +11,6 @@ for d in sys.argv[1:]:
         n = r["Name"]
         if "at::native" in n or "rocclr" in n:
             continue
-        short = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         print(f"  {short[:48]:48s} calls={int(r['Calls']):6d} avg_us={float(r['AverageNs'])/1e3:9.2f}"
               f" total_ms={float(r['TotalDurationNs'])/1e6:9.2f}")
