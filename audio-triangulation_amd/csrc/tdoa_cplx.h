@@ -1,0 +1,192 @@
+// tdoa_cplx.h -- packed-fp32 complex arithmetic for gfx950 (one f2 = one
+// 64-bit VGPR pair = re, im).  The compiler does not fold the re/im swaps of
+// "* i" and the conjugations of complex code into the VOP3P op_sel / neg
+// modifiers of v_pk_add_f32 / v_pk_fma_f32 (it materialises them with v_mov +
+// v_xor), so the primitives below pin one packed instruction each:
+//   op_sel[i]    picks the dword of source i that feeds the LOW result,
+//   op_sel_hi[i] the dword that feeds the HIGH result (default 1 = high),
+//   neg_lo / neg_hi negate source i's input to the low / high result.
+// Used by the config-2 kernel (tdoa_phat1024.hip) only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "tdoa_fft32.h"
+
+namespace {
+
+#define TDOA_PK(name, mnemonic, mods)                                      \
+    __device__ __forceinline__ f2 name(f2 a, f2 b)                         \
+    {                                                                      \
+        f2 r;                                                              \
+        asm(mnemonic " %0, %1, %2 " mods : "=v"(r) : "v"(a), "v"(b));      \
+        return r;                                                          \
+    }
+// a + conj(b), a - conj(b)
+TDOA_PK(c_addconj, "v_pk_add_f32", "neg_hi:[0,1]")
+TDOA_PK(c_subconj, "v_pk_add_f32", "neg_lo:[0,1]")
+// a - i b = (a.x + b.y, a.y - b.x);  a + i b = (a.x - b.y, a.y + b.x)
+TDOA_PK(c_add_mi, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]")
+TDOA_PK(c_add_i, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]")
+// -i (a - b) = (a.y - b.y, b.x - a.x);  i (a - b) = (b.y - a.y, a.x - b.x)
+TDOA_PK(c_sub_mi, "v_pk_add_f32", "op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]")
+TDOA_PK(c_sub_i, "v_pk_add_f32", "op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]")
+// conj(a + i b) = (a.x - b.y, -a.y - b.x);  conj(a - i b) = (a.x + b.y, b.x - a.y)
+TDOA_PK(c_conj_add_i, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[1,1]")
+TDOA_PK(c_conj_add_mi, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0]")
+#undef TDOA_PK
+
+// a * w
+__device__ __forceinline__ f2 c_mul(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+// a * conj(w)
+__device__ __forceinline__ f2 c_mulconj(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(r)
+        : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+// conj(a) * b
+__device__ __forceinline__ f2 c_conjmul(f2 a, f2 b)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "v"(b), "v"(t));
+    return r;
+}
+// the same with the twiddle in an SGPR pair (compile-time constants)
+__device__ __forceinline__ f2 c_mul_s(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+__device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+
+// -(a * w), -(a * conj(w))  (negated twiddle products, SGPR twiddle)
+__device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+__device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w)
+{
+    f2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,1]"
+        : "=v"(r)
+        : "v"(a), "s"(w), "v"(t));
+    return r;
+}
+// -i x = (x.y, -x.x);  i x = (-x.y, x.x)
+__device__ __forceinline__ f2 c_mi(f2 x)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ f2 c_i(f2 x)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_lo:[0,1]" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// x / max(|x|, sqrt(e2)):  (x.x^2, x.y^2) -> |x|^2 in both dwords -> rsq -> scale
+__device__ __forceinline__ f2 c_unit(f2 x, float e2)
+{
+    f2 t, s;
+    asm("v_pk_mul_f32 %0, %1, %1" : "=v"(t) : "v"(x));
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(s) : "v"(t));
+    const float r = __builtin_amdgcn_rsqf(fmaxf(s.x, e2));
+    f2 y;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(f2{r, r}));
+    return y;
+}
+
+// W_32^k = e^{-2 pi i k / 32}, k = 1..7 (the others by symmetry)
+__device__ __forceinline__ f2 w32c(int k)
+{
+    constexpr float C[8] = {1.0f,         0.98078528f, 0.92387953f, 0.83146961f,
+                            0.70710678f,  0.55557023f, 0.38268343f, 0.19509032f};
+    return f2{C[k], -C[8 - k]};
+}
+
+// (a - b) * W_32^{+-k}: the twiddle of one radix-2 DIF butterfly
+template <bool INV>
+__device__ __forceinline__ f2 dif_tw(f2 a, f2 b, int k)
+{
+    if (k == 0)
+        return a - b;
+    if (k == 8)
+        return INV ? c_sub_i(a, b) : c_sub_mi(a, b);
+    if (k < 8)
+        return INV ? c_mulconj_s(a - b, w32c(k)) : c_mul_s(a - b, w32c(k));
+    // W^k = -conj(W^{16-k})
+    return INV ? c_mul_s(b - a, w32c(16 - k)) : c_mulconj_s(b - a, w32c(16 - k));
+}
+// x * W_32^{+-k} (no subtraction)
+template <bool INV>
+__device__ __forceinline__ f2 tw_only(f2 x, int k)
+{
+    if (k == 0)
+        return x;
+    if (k == 8)
+        return INV ? c_i(x) : c_mi(x);
+    if (k < 8)
+        return INV ? c_mulconj_s(x, w32c(k)) : c_mul_s(x, w32c(k));
+    return INV ? c_negmul_s(x, w32c(16 - k)) : c_negmulconj_s(x, w32c(16 - k));
+}
+
+// In-place radix-2 DIF DFT-32 on packed primitives: natural-order input, X[k]
+// ends in v[brev5(k)].  HALF_ZERO: inputs 16..31 are zero.
+template <bool INV, bool HALF_ZERO>
+__device__ __forceinline__ void fft32p(f2 (&v)[32])
+{
+#pragma unroll
+    for (int span = 16; span >= 1; span >>= 1) {
+#pragma unroll
+        for (int start = 0; start < 32; start += 2 * span) {
+#pragma unroll
+            for (int j = 0; j < span; j++) {
+                const int k = j * (16 / span);
+                if (HALF_ZERO && span == 16) {
+                    v[j + 16] = tw_only<INV>(v[j], k);
+                } else {
+                    const f2 a = v[start + j], b = v[start + j + span];
+                    v[start + j] = a + b;
+                    v[start + j + span] = dif_tw<INV>(a, b, k);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace

@@ -8,6 +8,7 @@
 #include <climits>
 
 #include "tdoa_device.h"
+#include "tdoa_fft32.h"
 #include "tdoa_internal.h"
 
 int tdoa_set_error(int code, const char *msg);
@@ -273,7 +274,6 @@ int hip_fail(hipError_t e, const char *what)
 //     the second DFT-32 evaluates just its outputs 0 and 31 per lane;
 //   * 2 frames per 192-thread workgroup (6 half-waves = 6 FFTs), persistent
 //     over frame pairs with the next pair's samples prefetched in registers.
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 #ifdef TDOA_DIAG
 // diagnostic build only: per-workgroup cycles per phase of k_gcc_phat_1024
@@ -290,64 +290,6 @@ __device__ unsigned long long g_diag_phat[1 << 16];
     } while (0)
 #endif
 
-__device__ __forceinline__ f2 cmulf(f2 a, f2 b)
-{
-    return f2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
-}
-__device__ __forceinline__ f2 conjf2(f2 a) { return f2{a.x, -a.y}; }
-__device__ __forceinline__ f2 times_i(f2 a) { return f2{-a.y, a.x}; }
-__device__ __forceinline__ f2 times_mi(f2 a) { return f2{a.y, -a.x}; }
-
-// cos / sin (2 pi k / 32), k = 0..15
-__device__ constexpr float COS32[16] = {
-    1.0f,         0.98078528f,  0.92387953f,  0.83146961f, 0.70710678f,  0.55557023f,
-    0.38268343f,  0.19509032f,  0.0f,         -0.19509032f, -0.38268343f, -0.55557023f,
-    -0.70710678f, -0.83146961f, -0.92387953f, -0.98078528f};
-__device__ constexpr float SIN32[16] = {
-    0.0f,        0.19509032f, 0.38268343f, 0.55557023f, 0.70710678f, 0.83146961f,
-    0.92387953f, 0.98078528f, 1.0f,        0.98078528f, 0.92387953f, 0.83146961f,
-    0.70710678f, 0.55557023f, 0.38268343f, 0.19509032f};
-
-// t * W_32^k (forward, W = e^{-2 pi i/32}) or * W_32^{-k} (inverse)
-template <bool INV>
-__device__ __forceinline__ f2 tw32(f2 t, int k)
-{
-    if (k == 0)
-        return t;
-    if (k == 8)
-        return INV ? times_i(t) : times_mi(t);
-    return cmulf(t, f2{COS32[k], INV ? SIN32[k] : -SIN32[k]});
-}
-
-__device__ constexpr int brev5(int k)
-{
-    return ((k & 1) << 4) | ((k & 2) << 2) | (k & 4) | ((k & 8) >> 2) | ((k & 16) >> 4);
-}
-
-// In-place radix-2 DIF DFT-32: natural-order input, X[k] ends in v[brev5(k)].
-// HALF_ZERO: inputs 16..31 are zero.
-template <bool INV, bool HALF_ZERO>
-__device__ __forceinline__ void fft32(f2 (&v)[32])
-{
-#pragma unroll
-    for (int span = 16; span >= 1; span >>= 1) {
-#pragma unroll
-        for (int start = 0; start < 32; start += 2 * span) {
-#pragma unroll
-            for (int j = 0; j < span; j++) {
-                const int k = j * (16 / span);
-                if (HALF_ZERO && span == 16) {
-                    v[j + 16] = tw32<INV>(v[j], k);
-                } else {
-                    const f2 a = v[start + j], b = v[start + j + span];
-                    v[start + j] = a + b;
-                    v[start + j + span] = tw32<INV>(a - b, k);
-                }
-            }
-        }
-    }
-}
-
 // element (row, col) of a 32 x 32 complex tile: 16-byte chunks XOR-swizzled by
 // row so that both row reads (b128) and column writes (b64) are conflict-free
 __device__ __forceinline__ int swz(int row, int col)
@@ -363,41 +305,6 @@ __device__ __forceinline__ f2 ldf2(const float *p, int k) { return f2{p[2 * k], 
 // increasing tuples per lane, then (max, first tuple) across the workgroup.
 constexpr int GSLOTS = 8;
 
-// (max value, first index) combine through one DPP lane move (no LDS round
-// trip).  Lanes whose row is outside ROWMASK keep their own value (old = src).
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void dpp_argmax(float &v, int &i)
-{
-    const int vb = __builtin_bit_cast(int, v);
-    const float ov =
-        __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(vb, vb, CTRL, ROWMASK, 0xF, false));
-    const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWMASK, 0xF, false);
-    if (ov > v || (ov == v && oi < i)) {
-        v = ov;
-        i = oi;
-    }
-}
-// within each 16-lane row: xor 1, xor 2 (quad_perm), half-row mirror, row mirror
-__device__ __forceinline__ void row_argmax(float &v, int &i)
-{
-    dpp_argmax<0xB1, 0xF>(v, i);
-    dpp_argmax<0x4E, 0xF>(v, i);
-    dpp_argmax<0x141, 0xF>(v, i);
-    dpp_argmax<0x140, 0xF>(v, i);
-}
-// whole wave -> lane 63 (row_bcast:15 into rows 1, 3; row_bcast:31 into rows 2, 3)
-__device__ __forceinline__ void wave_argmax_to63(float &v, int &i)
-{
-    row_argmax(v, i);
-    dpp_argmax<0x142, 0xA>(v, i);
-    dpp_argmax<0x143, 0xC>(v, i);
-}
-// each 32-lane half-wave -> its lane 31 / 63
-__device__ __forceinline__ void half_argmax_to31(float &v, int &i)
-{
-    row_argmax(v, i);
-    dpp_argmax<0x142, 0xA>(v, i);
-}
 __device__ __forceinline__ void grid_tail(const tdoa_kparams &kp, const tdoa_kout &out,
                                           const float *wsc, const int64_t *gfr, float *gredv,
                                           int *gredi, int ns, uint32_t *tups)
@@ -753,8 +660,14 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
 bool tdoa_gcc_phat_needs_split(int M, int N) { return M > 3 || N > 2048; }
 
 // the N = 1024, 3-mic kernel runs the grid solve itself (grid_tail)
+bool tdoa_phat1024_fits(const tdoa_kparams &kp);
+int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
+                         int64_t B, float phat_eps, void *stream);
+
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp)
 {
+    if (tdoa_phat1024_fits(kp))
+        return true;
     // the tuple table is staged in the 48 KiB of FFT buffers
     return kp.M == 3 && kp.N == 1024 && kp.S <= 63 && kp.TW == 1 && kp.U <= 6 * 1024 * 2;
 }
@@ -771,6 +684,8 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
     if (!kp.tw || !kp.tw2)
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
+    if (tdoa_phat1024_fits(kp))
+        return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
     if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
         return tdoa_launch_gcc_phat_split(kp, out, frames, B,
                                           eps2 * 1152921504606846976.0f /* 2^60: int16 units */,

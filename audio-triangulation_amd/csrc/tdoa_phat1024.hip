@@ -1,0 +1,594 @@
+// tdoa_phat1024.hip -- GCC-PHAT metric kernel for BASELINE config 2
+// (3 mics x 1024-sample frames, L = 2048), see DESIGN.md "k_phat1024".
+//
+// One frame per 32-lane half-wave; the three mics of the frame run in the same
+// lanes, so no spectrum ever crosses a wave and the kernel has no workgroup
+// barrier after the table staging.  The work of a frame is issued as two
+// independent FFT streams at a time (mic 0 | mic 1, pair (0,1) inverse | mic 2
+// forward, pair (0,2) | pair (1,2)), each with its own transpose tile, so one
+// wave per SIMD has the instruction-level parallelism to cover LDS latency.
+//
+// Per mic m (rolling_buffer.c:64-66, buffer.c:13-16, buffer.c:4-11 front end):
+//   z[n] = x[2n] + i x[2n+1]  (n < 512; the upper half is the zero padding)
+//   Z = FFT_1024(z) as 32 x 32: DFT-32 over n1 in registers (lane = residue
+//       column n2 = res(lane)), twiddle W_1024^{n2 k1}, transpose through a
+//       private padded LDS tile (row stride 264 B: b64 writes and reads are
+//       bank-conflict free with no swizzle), DFT-32 over n2.
+//       Lane l then holds Z[res + 32 k2], k2 = 0..31.
+//   Real-FFT split X[b] (b <-> N - b): lanes l, l^1 hold the partner residues
+//       res, 32 - res; they swap their upper 16 registers by DPP so that the
+//       partner of register k is register 31 - k in the same lane (lane 0 --
+//       residue 0, self-paired with two fixed points 0 and 512 -- rotates its
+//       upper half instead and keeps bin 512 in a 33rd register; lane 1 --
+//       residue 16, self-paired -- keeps its registers).
+//   PHAT factored per mic: U_m = X_m / max(|X_m|, sqrt(e)), so
+//       R_ij = conj(U_i) U_j is the unit cross-spectrum.  Equal to the oracle's
+//       R / max(|R|, eps) whenever |X_i|, |X_j| >= sqrt(eps) (every nonzero bin
+//       of an integer frame in practice; an all-zero bin gives 0 either way).
+// Per pair (0,1), (0,2), (1,2) (sample_compute.h:120-122 order):
+//   Y[b] = (R[b] + R*[N-b]) + i (R[b] - R*[N-b]) W_2048^{-b}   (in-lane pairs)
+//   swap back to residue columns, y = IFFT_1024(Y) pruned to the outputs
+//   n = n1 (+992) that hold lags -S..S, argmax + lag prior (correlations.c:20-33
+//   semantics on float scores), gate (sample_compute.h:124-134).
+// Per wave and iteration: the grid solve of vga_heatmap.h:99-108 for its two
+// frames at once (lanes split the distinct lag tuples, one b64 gather per pair
+// reads both frames' weighted scores).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+
+#include "tdoa_cplx.h"
+#include "tdoa_internal.h"
+
+int tdoa_set_error(int code, const char *msg);
+
+namespace {
+
+constexpr int P1K_ROW = 264;              // tile row stride, bytes (32 complex + 8 B pad)
+constexpr int P1K_TILE = 32 * P1K_ROW;    // 8448 B: one transpose of one half-wave
+constexpr int P1K_KPAD = 128;             // lag slots per pair in the grid score table
+constexpr int P1K_WAVE_LDS = 4 * P1K_TILE;  // two tiles per half-wave
+
+// residue column held by lane l of a half-wave: lanes (2j, 2j+1) hold the
+// partner residues (j, 32 - j); lanes 0, 1 the self-paired residues 0, 16
+__device__ __forceinline__ int lane_res(int l)
+{
+    return l < 2 ? l * 16 : ((l & 1) ? 32 - (l >> 1) : (l >> 1));
+}
+
+__device__ __forceinline__ float dpp_xor1(float v)
+{
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ f2 dpp_xor1(f2 v) { return f2{dpp_xor1(v.x), dpp_xor1(v.y)}; }
+typedef short v2s_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void better(float &bv, int &bu, float ov, int ou)
+{
+    if (ov > bv || (ov == bv && ou < bu)) {
+        bv = ov;
+        bu = ou;
+    }
+}
+
+// sum over the 32 lanes of each half-wave
+__device__ __forceinline__ int hsum32(int s)
+{
+    s += __builtin_amdgcn_mov_dpp(s, 0xB1, 0xF, 0xF, false);   // xor 1
+    s += __builtin_amdgcn_mov_dpp(s, 0x4E, 0xF, 0xF, false);   // xor 2
+    s += __builtin_amdgcn_mov_dpp(s, 0x141, 0xF, 0xF, false);  // half-row mirror
+    s += __builtin_amdgcn_mov_dpp(s, 0x140, 0xF, 0xF, false);  // row mirror
+    s += __shfl_xor(s, 16, 32);
+    return s;
+}
+
+__device__ __forceinline__ f2 lds_f2(const char *base, int off)
+{
+    return *reinterpret_cast<const f2 *>(base + off);
+}
+__device__ __forceinline__ void sts_f2(char *base, int off, f2 v)
+{
+    *reinterpret_cast<f2 *>(base + off) = v;
+}
+
+__device__ __forceinline__ f2 unit(f2 x, float e2)
+{
+    return x * __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
+}
+
+struct Lane {
+    int lane;         // 0..31 within the half-wave
+    int res;          // residue column
+    bool is0, is1;    // the self-paired lanes
+    char *tileA;      // this half-wave's two transpose tiles
+    char *tileB;
+    const char *twm;  // [k][r] W_1024^{r k}
+    const char *tw2;  // [k][r] W_2048^{r + 32 k}, k < 16
+    const char *win;  // [w] (W[2w], W[2w+1]) / 128
+};
+
+// integer front end of one mic row (16 words per lane) -> v[t] = z[res + 32 t]
+__device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16], f2 (&v)[32])
+{
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+        s = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_t, w[t]), v2s_t{1, 1}, s, false);
+    s = hsum32(s);
+    // floor-mean DC (int64 arithmetic shift == floor), low byte of x - off
+    // (x <<= 8 keeps only it), ((s << 8) * W) >> 15 == floor(s * W / 128):
+    // exact in fp32, samples stay in int16 units
+    const uint32_t off = (uint32_t)(s >> 10) & 0xFFu;
+    const uint32_t off2 = off | (off << 16);
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const uint32_t d = (w[t] | 0x01000100u) - off2;  // no borrow across the halves
+        const float s0 = (float)(int8_t)(d & 0xFFu);
+        const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+        const f2 wf = lds_f2(L.win, 8 * L.res + 256 * t);
+        v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
+    }
+}
+
+// first half of a 32 x 32 FFT_1024 on a residue column: DFT-32 in registers,
+// twiddle W_1024^{-+res k}, column write into the tile
+template <bool INV, bool HALF_ZERO>
+__device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile)
+{
+    fft32p<INV, HALF_ZERO>(v);
+    const int wo = 8 * L.res;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        f2 x = v[brev5(k)];
+        if (k)
+            x = INV ? c_mulconj(x, lds_f2(L.twm, wo + 256 * k)) : c_mul(x, lds_f2(L.twm, wo + 256 * k));
+        sts_f2(tile, wo + P1K_ROW * k, x);
+    }
+}
+// second half: row read (row res) + forward DFT-32 -> V[k2] = Z[res + 32 k2]
+__device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 (&V)[33])
+{
+    f2 v[32];
+    const int ro = P1K_ROW * L.res;
+#pragma unroll
+    for (int n = 0; n < 32; n++)
+        v[n] = lds_f2(tile, ro + 8 * n);
+    fft32p<false, false>(v);
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        V[k] = v[brev5(k)];
+}
+// second half of the inverse, pruned: y[res] (y0) and y[res + 992] (y31)
+__device__ __forceinline__ void fft_row_inv(const Lane &L, const char *tile, f2 &y0, f2 &y31)
+{
+    f2 v[32];
+    const int ro = P1K_ROW * L.res;
+#pragma unroll
+    for (int n = 0; n < 32; n++)
+        v[n] = lds_f2(tile, ro + 8 * n);
+    // outputs n2 = 0 and 31 of the second DFT-32: y0 = sum v[r],
+    // y31 = sum v[r] W_32^r = sum_{r<16} (v[r] - v[r+16]) W_32^r
+    f2 a[16], d[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        a[r] = v[r] + v[r + 16];
+        d[r] = tw_only<false>(v[r] - v[r + 16], r);
+    }
+#pragma unroll
+    for (int h = 8; h >= 1; h >>= 1)
+#pragma unroll
+        for (int r = 0; r < h; r++) {
+            a[r] = a[r] + a[r + h];
+            d[r] = d[r] + d[r + h];
+        }
+    y0 = a[0];
+    y31 = d[0];
+}
+
+// real-FFT split + per-bin unit normalisation, in place: residue column ->
+// paired layout (V[k], V[31-k] hold bins b, N-b; V[32] = bin 512 on lane 0)
+__device__ __forceinline__ void split_unit(const Lane &L, f2 (&V)[33], float e2)
+{
+    V[32] = c_unit(conjf2(V[16]), e2);  // X[512] = conj(Z[512]) (x2), lane 0
+#pragma unroll
+    for (int j = 16; j < 32; j++) {  // ascending: lane 0 reads V[j+1] before it changes
+        const f2 t = dpp_xor1(V[j]);
+        const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
+        V[j] = (L.is0 || L.is1) ? own : t;
+    }
+    const int wo = 8 * L.res;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const f2 A = V[k], Bv = V[31 - k];
+        const f2 w = lds_f2(L.tw2, wo + 256 * k);  // W_2048^b
+        const f2 e = c_addconj(A, Bv);
+        const f2 od = c_mul(c_subconj(A, Bv), w);
+        // X[b] = e - i W^b d,  X[N-b] = conj(e + i W^b d)   (both x2; PHAT is scale-free)
+        V[k] = c_unit(c_add_mi(e, od), e2);
+        V[31 - k] = c_unit(c_conj_add_i(e, od), e2);
+    }
+}
+
+// U <- conj(U) V  (unit cross spectrum R_ij = conj(U_i) U_j, paired layout incl. slot 32)
+__device__ __forceinline__ void cross(f2 (&U)[33], const f2 (&V)[33])
+{
+#pragma unroll
+    for (int k = 0; k < 33; k++)
+        U[k] = c_conjmul(U[k], V[k]);
+}
+
+// packed inverse input Y from the cross spectrum R (paired layout), in place,
+// then back to residue columns
+__device__ __forceinline__ void pretwiddle(const Lane &L, f2 (&V)[33])
+{
+    const int wo = 8 * L.res;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const f2 Rk = V[k], Rn = V[31 - k];
+        const f2 w = lds_f2(L.tw2, wo + 256 * k);
+        const f2 s = c_addconj(Rk, Rn);
+        const f2 q = c_mulconj(c_subconj(Rk, Rn), w);
+        V[k] = c_add_i(s, q);              // s + i q
+        V[31 - k] = c_conj_add_mi(s, q);   // conj(s - i q)
+    }
+    const f2 Ye = f2{2.0f * V[32].x, -2.0f * V[32].y};  // Y[512] = 2 conj(R[512])
+#pragma unroll
+    for (int j = 31; j >= 16; j--) {  // descending: lane 0 reads V[j-1] before it changes
+        const f2 t = dpp_xor1(V[j]);
+        const f2 own = L.is0 ? (j == 16 ? Ye : V[j - 1]) : V[j];
+        V[j] = (L.is0 || L.is1) ? own : t;
+    }
+}
+
+__device__ __forceinline__ void copy32(f2 (&d)[32], const f2 (&s)[33])
+{
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        d[k] = s[k];
+}
+
+}  // namespace
+
+#ifdef TDOA_DIAG
+// diagnostic build only: per-wave cycles per phase of k_phat1024
+__device__ unsigned long long g_diag_p1k[1 << 16];
+#define P1K_MARK(i)                                                 \
+    do {                                                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph_acc[i] += t_ - ph_t;                                     \
+        ph_t = t_;                                                  \
+    } while (0)
+#else
+#define P1K_MARK(i) \
+    do {            \
+    } while (0)
+#endif
+
+// NW waves per workgroup, 2 frames per wave (one per half-wave) per iteration.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout out,
+                                                      const int16_t *__restrict__ frames,
+                                                      int64_t B, float e2)
+{
+    constexpr int N = 1024, P = 3, NF = 2 * NW, NT = NW * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *tiles = smem;                         // [NW][P1K_WAVE_LDS]
+    char *twm = tiles + NW * P1K_WAVE_LDS;      // [32][32] f2
+    char *tw2 = twm + 32 * 32 * 8;              // [16][32] f2
+    char *win = tw2 + 16 * 32 * 8;              // [512] f2
+    float *prior = (float *)(win + 512 * 8);    // [128]
+    uint32_t *tups = (uint32_t *)(prior + 128); // [U] distinct lag tuples (grid), resident
+
+    const int tid = threadIdx.x, wave = tid >> 6, hw = (tid >> 5) & 1, lane64 = tid & 63;
+    Lane L;
+    L.lane = tid & 31;
+    L.res = lane_res(L.lane);
+    L.is0 = L.lane == 0;
+    L.is1 = L.lane == 1;
+    char *wtiles = tiles + wave * P1K_WAVE_LDS;
+    L.tileA = wtiles + hw * P1K_TILE;
+    L.tileB = wtiles + (2 + hw) * P1K_TILE;
+    L.twm = twm;
+    L.tw2 = tw2;
+    L.win = win;
+
+#ifdef TDOA_DIAG
+    unsigned long long ph_acc[16] = {};
+    unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#endif
+    const int K = kp.K, S = kp.S;
+    for (int e = tid; e < 1024; e += NT) {
+        const int k = e >> 5, r = e & 31, i = (k * r) & (N - 1);
+        ((f2 *)twm)[e] = f2{kp.tw[2 * i], kp.tw[2 * i + 1]};
+    }
+    for (int e = tid; e < 512; e += NT) {
+        const int b = (e & 31) + 32 * (e >> 5);  // [k][r] -> b = r + 32 k
+        ((f2 *)tw2)[e] = f2{kp.tw2[2 * b], kp.tw2[2 * b + 1]};
+        ((f2 *)win)[e] = f2{(float)kp.window[2 * e] * (1.0f / 128.0f),
+                            (float)kp.window[2 * e + 1] * (1.0f / 128.0f)};
+    }
+    for (int e = tid; e < K; e += NT)
+        prior[e] = kp.prior[e];
+    const bool do_grid = out.cell || out.xy || out.max_Lf;
+    if (do_grid)
+        for (int e = tid; e < kp.U; e += NT)
+            tups[e] = kp.tuples[e];
+    __syncthreads();
+    P1K_MARK(0);
+
+    const float invL = 1.0f / 2048.0f;
+    // this lane's four candidate lags: y[res+992] -> 2 res - 64 (+1), y[res] -> 2 res (+1),
+    // in ascending lag order (first max wins, correlations.c:20-23)
+    const int la = 2 * L.res, lb = 2 * L.res - 64;
+    const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
+    const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
+
+    // frame words of this half-wave's frame, next iteration's prefetched
+    uint32_t w0[16], w1[16], w2[16], n0[16], n1[16], n2[16];
+    // unconditional loads (a frame past the batch re-reads the last one and
+    // stores nothing): a per-load select would serialise the loads on vmcnt
+    auto fetch = [&](uint32_t(&w)[16], int64_t fr, int m) {
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(
+            frames + ((fr < B ? fr : B - 1) * 3 + m) * (int64_t)N) + L.res;
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            w[t] = __builtin_nontemporal_load(row + 32 * t);
+    };
+    {
+        const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
+        fetch(n0, f, 0);
+        fetch(n1, f, 1);
+        fetch(n2, f, 2);
+    }
+    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += (int64_t)gridDim.x * NF) {
+        const int64_t f = base + 2 * wave + hw;
+        const bool live = f < B;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            w0[t] = n0[t];
+            w1[t] = n1[t];
+            w2[t] = n2[t];
+        }
+        {
+            const int64_t fn = f + (int64_t)gridDim.x * NF;
+            fetch(n0, fn, 0);
+            fetch(n1, fn, 1);
+            fetch(n2, fn, 2);
+        }
+#ifdef TDOA_DIAG
+        ph_acc[15]++;
+#endif
+
+        float wv[3][4];
+        int best[3];
+        // argmax + prior + outputs of pair p from y[res] (y0) and y[res+992] (y31)
+        auto finish_pair = [&](int p, f2 y0, f2 y31) {
+            const float cv[4] = {y31.x * invL, y31.y * invL, y0.x * invL, y0.y * invL};
+            float bv = -INFINITY;
+            int bk = INT_MAX;
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (ok[c] && (cv[c] > bv || bk == INT_MAX)) {
+                    bv = cv[c];
+                    bk = ck[c];
+                }
+            half_argmax_to31(bv, bk);
+            const int b0 = __builtin_amdgcn_readlane(bk, 31), b1 = __builtin_amdgcn_readlane(bk, 63);
+            bk = hw ? b1 : b0;  // uniform per half-wave even for NaN scores
+            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
+            best[p] = bk - S;
+            const size_t gb = (size_t)(f * P + p) * K;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int d = ck[c] > bk ? ck[c] - bk : bk - ck[c];
+                wv[p][c] = ok[c] ? cv[c] * prior[ok[c] ? d : 0] : 0.0f;
+                if (live && ok[c]) {
+                    if (out.scores_f)
+                        out.scores_f[gb + ck[c]] = cv[c];
+                    if (out.weighted_f)
+                        out.weighted_f[gb + ck[c]] = wv[p][c];
+                }
+            }
+            if (live && L.lane == 0)
+                out.lags[f * P + p] = bk - S;
+        };
+
+        // mic 0 | mic 1 forward, split + unit normalisation
+        f2 U0[33], U1[33], V[33], va[32], vb[32], y0, y31;
+        front_end(L, w0, va);
+        front_end(L, w1, vb);
+        fft_col<false, true>(L, va, L.tileA);
+        fft_col<false, true>(L, vb, L.tileB);
+        fft_row_fwd(L, L.tileA, U0);
+        fft_row_fwd(L, L.tileB, U1);
+        P1K_MARK(1);
+        split_unit(L, U0, e2);
+        split_unit(L, U1, e2);
+        P1K_MARK(2);
+        // pair (0,1) inverse | mic 2 forward
+#pragma unroll
+        for (int k = 0; k < 33; k++)
+            V[k] = U0[k];
+        cross(V, U1);
+        pretwiddle(L, V);
+        copy32(va, V);
+        front_end(L, w2, vb);
+        fft_col<true, false>(L, va, L.tileA);
+        fft_col<false, true>(L, vb, L.tileB);
+        fft_row_inv(L, L.tileA, y0, y31);
+        fft_row_fwd(L, L.tileB, V);
+        finish_pair(0, y0, y31);
+        P1K_MARK(3);
+        split_unit(L, V, e2);
+        cross(U0, V);  // pair 1: (0, 2)
+        cross(U1, V);  // pair 2: (1, 2)
+        P1K_MARK(4);
+        // pair (0,2) | pair (1,2) inverse
+        pretwiddle(L, U0);
+        pretwiddle(L, U1);
+        copy32(va, U0);
+        copy32(vb, U1);
+        fft_col<true, false>(L, va, L.tileA);
+        fft_col<true, false>(L, vb, L.tileB);
+        f2 z0, z31;
+        fft_row_inv(L, L.tileA, y0, y31);
+        fft_row_inv(L, L.tileB, z0, z31);
+        finish_pair(1, y0, y31);
+        finish_pair(2, z0, z31);
+        if (live && L.lane == 0 && out.gate)
+            out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
+        P1K_MARK(5);
+
+        if (!do_grid)
+            continue;
+        // ---- grid solve of this wave's two frames (vga_heatmap.h:99-108): weighted
+        // scores -> [p][k] (frame of half-wave 0, frame of half-wave 1) in the wave's
+        // tile space, lanes split the tuples, (max L, first tuple) per frame
+        float *wsc = (float *)wtiles;  // [P][KPAD][2]
+#pragma unroll
+        for (int p = 0; p < P; p++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (ok[c])
+                    wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
+        float gv0 = -INFINITY, gv1 = -INFINITY;
+        int gu0 = INT_MAX, gu1 = INT_MAX;
+        const f2 *ws2 = (const f2 *)wsc;
+#pragma unroll 4
+        for (int u = lane64; u < kp.U; u += 64) {
+            const uint32_t word = tups[u];
+            const f2 l0 = ws2[(int)(word & 0xFFu)];
+            const f2 l1 = ws2[P1K_KPAD + (int)((word >> 8) & 0xFFu)];
+            const f2 l2 = ws2[2 * P1K_KPAD + (int)((word >> 16) & 0xFFu)];
+            const f2 Lg = (l0 + l1) + l2;
+            if (Lg.x > gv0) {
+                gv0 = Lg.x;
+                gu0 = u;
+            }
+            if (Lg.y > gv1) {
+                gv1 = Lg.y;
+                gu1 = u;
+            }
+        }
+        wave_argmax_to63(gv0, gu0);
+        wave_argmax_to63(gv1, gu1);
+        if (lane64 == 63) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int64_t fs = base + 2 * wave + h;
+                int ui = h ? gu1 : gu0;
+                const float v = h ? gv1 : gv0;
+                if (fs < B) {
+                    if (ui < 0 || ui >= kp.U)  // every L compared false (NaN scores)
+                        ui = 0;
+                    const int cell = kp.tuple_cell[ui];
+                    if (out.cell)
+                        out.cell[fs] = cell;
+                    if (out.max_Lf)
+                        out.max_Lf[fs] = v;
+                    if (out.xy) {
+                        const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+                        out.xy[2 * fs] = (float)(cx - kp.half_w) / kp.grid_scale;
+                        out.xy[2 * fs + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+                    }
+                }
+            }
+        }
+        P1K_MARK(6);
+    }
+#ifdef TDOA_DIAG
+    if ((tid & 63) == 0 && (blockIdx.x * NW + wave) < 4096)
+        for (int i = 0; i < 16; i++)
+            g_diag_p1k[(blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
+#endif
+}
+
+#ifdef TDOA_DIAG
+extern "C" int tdoa_diag_fetch_p1k(unsigned long long *host, int n)
+{
+    if (n > (1 << 16))
+        n = 1 << 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_p1k), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif
+
+// --------------------------------------------------------------- host side
+namespace {
+template <int NW>
+constexpr size_t p1k_lds(int U)
+{
+    return (size_t)NW * P1K_WAVE_LDS + 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4 + (size_t)U * 4;
+}
+
+int g_p1k_waves = -1;  // 0: use the generic kernels (A/B), else NW
+
+template <int NW>
+int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+               float e2, hipStream_t st)
+{
+    const size_t lds = p1k_lds<NW>(kp.U);
+    static int c_dev = -1, c_resident = 0;
+    static size_t c_lds = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != c_dev || lds != c_lds) {
+        int per_cu = 0, cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phat1024<NW>, NW * 64, lds);
+        c_resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+        c_dev = dev;
+        c_lds = lds;
+    }
+    constexpr int NF = 2 * NW;
+    const int64_t groups = (B + NF - 1) / NF;
+    const int64_t iters = (groups + c_resident - 1) / c_resident;
+    const int64_t grid = (groups + iters - 1) / iters;
+    hipLaunchKernelGGL(k_phat1024<NW>, dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames,
+                       B, e2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "k_phat1024 launch: %s", hipGetErrorString(e));
+        return tdoa_set_error(-2, buf);
+    }
+    return 0;
+}
+}  // namespace
+
+// config-2 shape (M = 3, N = 1024, S <= 63) with a tuple table that fits the tail
+bool tdoa_phat1024_fits(const tdoa_kparams &kp)
+{
+    if (g_p1k_waves < 0) {
+        const char *s = getenv("TDOA_PHAT1024_WAVES");
+        g_p1k_waves = s ? atoi(s) : 4;
+        if (g_p1k_waves != 0 && g_p1k_waves != 4 && g_p1k_waves != 8)
+            g_p1k_waves = 8;
+    }
+    if (g_p1k_waves == 0 || kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1)
+        return false;
+    // grid scores of a wave's two frames live in its tiles: [3][KPAD] f2 = 3 KiB
+    static_assert(3 * P1K_KPAD * 8 <= P1K_WAVE_LDS, "grid scores exceed the wave's tiles");
+    if (g_p1k_waves == 8)
+        return p1k_lds<8>(kp.U) <= 160 * 1024;
+    return p1k_lds<4>(kp.U) <= 160 * 1024;
+}
+
+int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
+                         int64_t B, float phat_eps, void *stream)
+{
+    // per-mic clamp: |X_m| >= sqrt(eps) in the oracle's units (x / 2^15, X / 2),
+    // i.e. |X|^2 >= eps * 2^32 in the kernel's int16 units with the split's factor 2
+    float e2 = phat_eps * 4294967296.0f;
+    if (!(e2 >= 1e-30f))
+        e2 = 1e-30f;
+    hipStream_t st = (hipStream_t)stream;
+    return g_p1k_waves == 4 ? launch_p1k<4>(kp, out, frames, B, e2, st)
+                            : launch_p1k<8>(kp, out, frames, B, e2, st);
+}
