@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #define TDOA_MAX_PAIRS 28  // 8 mics
 #define TDOA_MAX_MICS_K 8
 #define TDOA_LS_ITERS 10   // least-squares refinement steps (tdoa_ls.hip)
@@ -42,6 +44,8 @@ struct tdoa_kparams {
     const float *tw;           // GCC_PHAT: e^{-2 pi i k/N}, k < N   (re, im)
     const float *tw2;          // GCC_PHAT: e^{-2 pi i k/2N}, k <= N (re, im)
     const uint8_t *lut;        // [P][G] lag index per cell (heat map)
+    const void *p1k_img;       // config-2 GCC-PHAT kernel: its LDS table image (16-B units)
+    int32_t p1k_img_bytes;
     // least-squares refinement (tdoa_ls.hip)
     const float *mic_xy;       // [M][2] metres
     float fs, c, height;
@@ -117,6 +121,11 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
 // GCC-PHAT shapes the fused kernels cannot hold (M > 3 or N > 2048): two
 // passes per chunk of frames through a spectrum scratch (tdoa_phat_split.hip)
 bool tdoa_gcc_phat_needs_split(int M, int N);
+// config-2 GCC-PHAT kernel (tdoa_phat1024.hip): host-built LDS table image
+// from the twiddles ([N] e^{-2 pi i k/N} then [N+1] e^{-2 pi i k/2N}),
+// Q15 window, lag prior and distinct lag tuples; empty if the shape differs
+void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
+                         const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img);
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
 int tdoa_launch_gcc_phat_split(const tdoa_kparams &kp, const tdoa_kout &out,
                                const int16_t *frames, int64_t B, float eps2_int16,

@@ -50,7 +50,11 @@ namespace {
 constexpr int P1K_ROW = 264;              // tile row stride, bytes (32 complex + 8 B pad)
 constexpr int P1K_TILE = 32 * P1K_ROW;    // 8448 B: one transpose of one half-wave
 constexpr int P1K_KPAD = 128;             // lag slots per pair in the grid score table
-constexpr int P1K_WAVE_LDS = 4 * P1K_TILE;  // two tiles per half-wave
+template <bool DUAL>
+constexpr int p1k_wave_lds() { return (DUAL ? 4 : 2) * P1K_TILE; }  // tiles per wave
+constexpr int P1K_GB = 8;                 // grid tuples per lane per batch
+// LDS table image: twm [32][32] f2 | tw2 [16][32] f2 | win [512] f2 | prior [128] | tuples
+constexpr int P1K_IMG_FIXED = 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4;
 
 // residue column held by lane l of a half-wave: lanes (2j, 2j+1) hold the
 // partner residues (j, 32 - j); lanes 0, 1 the self-paired residues 0, 16
@@ -75,15 +79,17 @@ __device__ __forceinline__ void better(float &bv, int &bu, float ov, int ou)
     }
 }
 
-// sum over the 32 lanes of each half-wave
-__device__ __forceinline__ int hsum32(int s)
+// sum over the 32 lanes of each half-wave, VALU only (no LDS queue): row
+// all-reduce by DPP, row_bcast:15 into rows 1 and 3, then lanes 31 / 63
+__device__ __forceinline__ int hsum32(int s, int hw)
 {
     s += __builtin_amdgcn_mov_dpp(s, 0xB1, 0xF, 0xF, false);   // xor 1
     s += __builtin_amdgcn_mov_dpp(s, 0x4E, 0xF, 0xF, false);   // xor 2
     s += __builtin_amdgcn_mov_dpp(s, 0x141, 0xF, 0xF, false);  // half-row mirror
     s += __builtin_amdgcn_mov_dpp(s, 0x140, 0xF, 0xF, false);  // row mirror
-    s += __shfl_xor(s, 16, 32);
-    return s;
+    s += __builtin_amdgcn_update_dpp(0, s, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const int s0 = __builtin_amdgcn_readlane(s, 31), s1 = __builtin_amdgcn_readlane(s, 63);
+    return hw ? s1 : s0;
 }
 
 __device__ __forceinline__ f2 lds_f2(const char *base, int off)
@@ -101,6 +107,7 @@ __device__ __forceinline__ f2 unit(f2 x, float e2)
 }
 
 struct Lane {
+    int hw;           // half-wave of the wave
     int lane;         // 0..31 within the half-wave
     int res;          // residue column
     bool is0, is1;    // the self-paired lanes
@@ -111,14 +118,36 @@ struct Lane {
     const char *win;  // [w] (W[2w], W[2w+1]) / 128
 };
 
+// per-lane table values, read into registers at the start of a phase (before
+// its tile writes, which the compiler cannot prove disjoint from the tables)
+__device__ __forceinline__ void load_twm(const Lane &L, f2 (&tw)[32])  // W_1024^{res k}
+{
+#pragma unroll
+    for (int k = 1; k < 32; k++)
+        tw[k] = lds_f2(L.twm, 8 * L.res + 256 * k);
+}
+__device__ __forceinline__ void load_tw2(const Lane &L, f2 (&t2)[16])  // W_2048^{res + 32 k}
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        t2[k] = lds_f2(L.tw2, 8 * L.res + 256 * k);
+}
+__device__ __forceinline__ void load_win(const Lane &L, f2 (&wf)[16])  // W / 128 of words res + 32 t
+{
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+        wf[t] = lds_f2(L.win, 8 * L.res + 256 * t);
+}
+
 // integer front end of one mic row (16 words per lane) -> v[t] = z[res + 32 t]
-__device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16], f2 (&v)[32])
+__device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16], f2 (&v)[32],
+                                          const f2 (&wfa)[16])
 {
     int s = 0;
 #pragma unroll
     for (int t = 0; t < 16; t++)
         s = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_t, w[t]), v2s_t{1, 1}, s, false);
-    s = hsum32(s);
+    s = hsum32(s, L.hw);
     // floor-mean DC (int64 arithmetic shift == floor), low byte of x - off
     // (x <<= 8 keeps only it), ((s << 8) * W) >> 15 == floor(s * W / 128):
     // exact in fp32, samples stay in int16 units
@@ -129,15 +158,14 @@ __device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16]
         const uint32_t d = (w[t] | 0x01000100u) - off2;  // no borrow across the halves
         const float s0 = (float)(int8_t)(d & 0xFFu);
         const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
-        const f2 wf = lds_f2(L.win, 8 * L.res + 256 * t);
-        v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
+        v[t] = f2{floorf(s0 * wfa[t].x), floorf(s1 * wfa[t].y)};
     }
 }
 
 // first half of a 32 x 32 FFT_1024 on a residue column: DFT-32 in registers,
 // twiddle W_1024^{-+res k}, column write into the tile
 template <bool INV, bool HALF_ZERO>
-__device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile)
+__device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, const f2 (&tw)[32])
 {
     fft32p<INV, HALF_ZERO>(v);
     const int wo = 8 * L.res;
@@ -145,7 +173,7 @@ __device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile)
     for (int k = 0; k < 32; k++) {
         f2 x = v[brev5(k)];
         if (k)
-            x = INV ? c_mulconj(x, lds_f2(L.twm, wo + 256 * k)) : c_mul(x, lds_f2(L.twm, wo + 256 * k));
+            x = INV ? c_mulconj(x, tw[k]) : c_mul(x, tw[k]);
         sts_f2(tile, wo + P1K_ROW * k, x);
     }
 }
@@ -191,7 +219,7 @@ __device__ __forceinline__ void fft_row_inv(const Lane &L, const char *tile, f2 
 
 // real-FFT split + per-bin unit normalisation, in place: residue column ->
 // paired layout (V[k], V[31-k] hold bins b, N-b; V[32] = bin 512 on lane 0)
-__device__ __forceinline__ void split_unit(const Lane &L, f2 (&V)[33], float e2)
+__device__ __forceinline__ void split_unit(const Lane &L, f2 (&V)[33], float e2, const f2 (&t2)[16])
 {
     V[32] = c_unit(conjf2(V[16]), e2);  // X[512] = conj(Z[512]) (x2), lane 0
 #pragma unroll
@@ -200,11 +228,10 @@ __device__ __forceinline__ void split_unit(const Lane &L, f2 (&V)[33], float e2)
         const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
         V[j] = (L.is0 || L.is1) ? own : t;
     }
-    const int wo = 8 * L.res;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const f2 A = V[k], Bv = V[31 - k];
-        const f2 w = lds_f2(L.tw2, wo + 256 * k);  // W_2048^b
+        const f2 w = t2[k];  // W_2048^b
         const f2 e = c_addconj(A, Bv);
         const f2 od = c_mul(c_subconj(A, Bv), w);
         // X[b] = e - i W^b d,  X[N-b] = conj(e + i W^b d)   (both x2; PHAT is scale-free)
@@ -223,13 +250,12 @@ __device__ __forceinline__ void cross(f2 (&U)[33], const f2 (&V)[33])
 
 // packed inverse input Y from the cross spectrum R (paired layout), in place,
 // then back to residue columns
-__device__ __forceinline__ void pretwiddle(const Lane &L, f2 (&V)[33])
+__device__ __forceinline__ void pretwiddle(const Lane &L, f2 (&V)[33], const f2 (&t2)[16])
 {
-    const int wo = 8 * L.res;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const f2 Rk = V[k], Rn = V[31 - k];
-        const f2 w = lds_f2(L.tw2, wo + 256 * k);
+        const f2 w = t2[k];
         const f2 s = c_addconj(Rk, Rn);
         const f2 q = c_mulconj(c_subconj(Rk, Rn), w);
         V[k] = c_add_i(s, q);              // s + i q
@@ -269,15 +295,17 @@ __device__ unsigned long long g_diag_p1k[1 << 16];
 #endif
 
 // NW waves per workgroup, 2 frames per wave (one per half-wave) per iteration.
-template <int NW>
+// DUAL: two FFT streams per half-wave (two tiles each); else one at a time.
+template <int NW, bool DUAL>
 __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout out,
                                                       const int16_t *__restrict__ frames,
                                                       int64_t B, float e2)
 {
     constexpr int N = 1024, P = 3, NF = 2 * NW, NT = NW * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *tiles = smem;                         // [NW][P1K_WAVE_LDS]
-    char *twm = tiles + NW * P1K_WAVE_LDS;      // [32][32] f2
+    constexpr int WAVE_LDS = p1k_wave_lds<DUAL>();
+    char *tiles = smem;                         // [NW][WAVE_LDS]
+    char *twm = tiles + NW * WAVE_LDS;          // [32][32] f2
     char *tw2 = twm + 32 * 32 * 8;              // [16][32] f2
     char *win = tw2 + 16 * 32 * 8;              // [512] f2
     float *prior = (float *)(win + 512 * 8);    // [128]
@@ -285,13 +313,14 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
 
     const int tid = threadIdx.x, wave = tid >> 6, hw = (tid >> 5) & 1, lane64 = tid & 63;
     Lane L;
+    L.hw = hw;
     L.lane = tid & 31;
     L.res = lane_res(L.lane);
     L.is0 = L.lane == 0;
     L.is1 = L.lane == 1;
-    char *wtiles = tiles + wave * P1K_WAVE_LDS;
+    char *wtiles = tiles + wave * WAVE_LDS;
     L.tileA = wtiles + hw * P1K_TILE;
-    L.tileB = wtiles + (2 + hw) * P1K_TILE;
+    L.tileB = DUAL ? wtiles + (2 + hw) * P1K_TILE : L.tileA;
     L.twm = twm;
     L.tw2 = tw2;
     L.win = win;
@@ -301,33 +330,11 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
     unsigned long long ph_t = __builtin_amdgcn_s_memtime();
 #endif
     const int K = kp.K, S = kp.S;
-    for (int e = tid; e < 1024; e += NT) {
-        const int k = e >> 5, r = e & 31, i = (k * r) & (N - 1);
-        ((f2 *)twm)[e] = f2{kp.tw[2 * i], kp.tw[2 * i + 1]};
-    }
-    for (int e = tid; e < 512; e += NT) {
-        const int b = (e & 31) + 32 * (e >> 5);  // [k][r] -> b = r + 32 k
-        ((f2 *)tw2)[e] = f2{kp.tw2[2 * b], kp.tw2[2 * b + 1]};
-        ((f2 *)win)[e] = f2{(float)kp.window[2 * e] * (1.0f / 128.0f),
-                            (float)kp.window[2 * e + 1] * (1.0f / 128.0f)};
-    }
-    for (int e = tid; e < K; e += NT)
-        prior[e] = kp.prior[e];
     const bool do_grid = out.cell || out.xy || out.max_Lf;
-    if (do_grid)
-        for (int e = tid; e < kp.U; e += NT)
-            tups[e] = kp.tuples[e];
-    __syncthreads();
-    P1K_MARK(0);
+    const int Upad = (kp.U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
 
-    const float invL = 1.0f / 2048.0f;
-    // this lane's four candidate lags: y[res+992] -> 2 res - 64 (+1), y[res] -> 2 res (+1),
-    // in ascending lag order (first max wins, correlations.c:20-23)
-    const int la = 2 * L.res, lb = 2 * L.res - 64;
-    const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
-    const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
-
-    // frame words of this half-wave's frame, next iteration's prefetched
+    // frame words of this half-wave's frame (issued before the table staging so
+    // the first HBM round trip overlaps it), the next iteration's prefetched
     uint32_t w0[16], w1[16], w2[16], n0[16], n1[16], n2[16];
     // unconditional loads (a frame past the batch re-reads the last one and
     // stores nothing): a per-load select would serialise the loads on vmcnt
@@ -344,6 +351,26 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
         fetch(n1, f, 1);
         fetch(n2, f, 2);
     }
+
+    // host-built table image (tdoa_phat1024_image): twm | tw2 | win | prior | tuples
+    {
+        const uint4 *src = (const uint4 *)kp.p1k_img;
+        uint4 *dst = (uint4 *)twm;
+        const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
+#pragma unroll 8
+        for (int e = tid; e < n16; e += NT)
+            dst[e] = src[e];
+    }
+    __syncthreads();
+    P1K_MARK(0);
+
+    const float invL = 1.0f / 2048.0f;
+    // this lane's four candidate lags: y[res+992] -> 2 res - 64 (+1), y[res] -> 2 res (+1),
+    // in ascending lag order (first max wins, correlations.c:20-23)
+    const int la = 2 * L.res, lb = 2 * L.res - 64;
+    const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
+    const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
+
     for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += (int64_t)gridDim.x * NF) {
         const int64_t f = base + 2 * wave + hw;
         const bool live = f < B;
@@ -397,48 +424,108 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
                 out.lags[f * P + p] = bk - S;
         };
 
-        // mic 0 | mic 1 forward, split + unit normalisation
-        f2 U0[33], U1[33], V[33], va[32], vb[32], y0, y31;
-        front_end(L, w0, va);
-        front_end(L, w1, vb);
-        fft_col<false, true>(L, va, L.tileA);
-        fft_col<false, true>(L, vb, L.tileB);
-        fft_row_fwd(L, L.tileA, U0);
-        fft_row_fwd(L, L.tileB, U1);
-        P1K_MARK(1);
-        split_unit(L, U0, e2);
-        split_unit(L, U1, e2);
-        P1K_MARK(2);
-        // pair (0,1) inverse | mic 2 forward
+        f2 U0[33], U1[33], V[33], va[32], vb[32], y0, y31, z0, z31;
+        f2 tw[32], t2[16], wf[16];
+        if constexpr (DUAL) {
+            // mic 0 | mic 1 forward, split + unit normalisation
+            load_win(L, wf);
+            load_twm(L, tw);
+            front_end(L, w0, va, wf);
+            front_end(L, w1, vb, wf);
+            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_col<false, true>(L, vb, L.tileB, tw);
+            fft_row_fwd(L, L.tileA, U0);
+            fft_row_fwd(L, L.tileB, U1);
+            P1K_MARK(1);
+            load_tw2(L, t2);
+            split_unit(L, U0, e2, t2);
+            split_unit(L, U1, e2, t2);
+            P1K_MARK(2);
+            // pair (0,1) inverse | mic 2 forward
+            load_win(L, wf);
+            load_twm(L, tw);
 #pragma unroll
-        for (int k = 0; k < 33; k++)
-            V[k] = U0[k];
-        cross(V, U1);
-        pretwiddle(L, V);
-        copy32(va, V);
-        front_end(L, w2, vb);
-        fft_col<true, false>(L, va, L.tileA);
-        fft_col<false, true>(L, vb, L.tileB);
-        fft_row_inv(L, L.tileA, y0, y31);
-        fft_row_fwd(L, L.tileB, V);
-        finish_pair(0, y0, y31);
-        P1K_MARK(3);
-        split_unit(L, V, e2);
-        cross(U0, V);  // pair 1: (0, 2)
-        cross(U1, V);  // pair 2: (1, 2)
-        P1K_MARK(4);
-        // pair (0,2) | pair (1,2) inverse
-        pretwiddle(L, U0);
-        pretwiddle(L, U1);
-        copy32(va, U0);
-        copy32(vb, U1);
-        fft_col<true, false>(L, va, L.tileA);
-        fft_col<true, false>(L, vb, L.tileB);
-        f2 z0, z31;
-        fft_row_inv(L, L.tileA, y0, y31);
-        fft_row_inv(L, L.tileB, z0, z31);
-        finish_pair(1, y0, y31);
-        finish_pair(2, z0, z31);
+            for (int k = 0; k < 33; k++)
+                V[k] = U0[k];
+            cross(V, U1);
+            pretwiddle(L, V, t2);
+            copy32(va, V);
+            front_end(L, w2, vb, wf);
+            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_col<false, true>(L, vb, L.tileB, tw);
+            fft_row_inv(L, L.tileA, y0, y31);
+            fft_row_fwd(L, L.tileB, V);
+            finish_pair(0, y0, y31);
+            P1K_MARK(3);
+            load_tw2(L, t2);
+            split_unit(L, V, e2, t2);
+            cross(U0, V);  // pair 1: (0, 2)
+            cross(U1, V);  // pair 2: (1, 2)
+            P1K_MARK(4);
+            // pair (0,2) | pair (1,2) inverse
+            load_twm(L, tw);
+            pretwiddle(L, U0, t2);
+            pretwiddle(L, U1, t2);
+            copy32(va, U0);
+            copy32(vb, U1);
+            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_col<true, false>(L, vb, L.tileB, tw);
+            fft_row_inv(L, L.tileA, y0, y31);
+            fft_row_inv(L, L.tileB, z0, z31);
+            finish_pair(1, y0, y31);
+            finish_pair(2, z0, z31);
+        } else {
+            // one stream: at most three spectra live (U0, U1, V)
+            load_win(L, wf);
+            load_twm(L, tw);
+            front_end(L, w0, va, wf);
+            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_row_fwd(L, L.tileA, U0);
+            load_tw2(L, t2);
+            split_unit(L, U0, e2, t2);
+            load_win(L, wf);
+            load_twm(L, tw);
+            front_end(L, w1, va, wf);
+            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_row_fwd(L, L.tileA, U1);
+            load_tw2(L, t2);
+            split_unit(L, U1, e2, t2);
+            P1K_MARK(1);
+            load_twm(L, tw);
+#pragma unroll
+            for (int k = 0; k < 33; k++)
+                V[k] = U0[k];
+            cross(V, U1);  // pair 0: (0, 1)
+            pretwiddle(L, V, t2);
+            copy32(va, V);
+            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_row_inv(L, L.tileA, y0, y31);
+            finish_pair(0, y0, y31);
+            P1K_MARK(2);
+            load_win(L, wf);
+            load_twm(L, tw);
+            front_end(L, w2, va, wf);
+            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_row_fwd(L, L.tileA, V);
+            load_tw2(L, t2);
+            split_unit(L, V, e2, t2);
+            cross(U0, V);  // pair 1: (0, 2)
+            cross(U1, V);  // pair 2: (1, 2)
+            P1K_MARK(3);
+            load_twm(L, tw);
+            pretwiddle(L, U0, t2);
+            copy32(va, U0);
+            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_row_inv(L, L.tileA, y0, y31);
+            finish_pair(1, y0, y31);
+            P1K_MARK(4);
+            load_twm(L, tw);
+            pretwiddle(L, U1, t2);
+            copy32(va, U1);
+            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_row_inv(L, L.tileA, z0, z31);
+            finish_pair(2, z0, z31);
+        }
         if (live && L.lane == 0 && out.gate)
             out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
         P1K_MARK(5);
@@ -455,23 +542,41 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
             for (int c = 0; c < 4; c++)
                 if (ok[c])
                     wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
+        if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
+            wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
         float gv0 = -INFINITY, gv1 = -INFINITY;
         int gu0 = INT_MAX, gu1 = INT_MAX;
-        const f2 *ws2 = (const f2 *)wsc;
-#pragma unroll 4
-        for (int u = lane64; u < kp.U; u += 64) {
-            const uint32_t word = tups[u];
-            const f2 l0 = ws2[(int)(word & 0xFFu)];
-            const f2 l1 = ws2[P1K_KPAD + (int)((word >> 8) & 0xFFu)];
-            const f2 l2 = ws2[2 * P1K_KPAD + (int)((word >> 16) & 0xFFu)];
-            const f2 Lg = (l0 + l1) + l2;
-            if (Lg.x > gv0) {
-                gv0 = Lg.x;
-                gu0 = u;
+        const char *ws = (const char *)wsc;
+        // batches of GB tuples per lane; the next batch's tuple words are read
+        // while the current batch's gathers are in flight
+        uint32_t wd[P1K_GB];
+#pragma unroll
+        for (int j = 0; j < P1K_GB; j++)
+            wd[j] = tups[64 * j + lane64];
+        for (int u0 = 0; u0 < Upad; u0 += 64 * P1K_GB) {
+            f2 Lg[P1K_GB];
+#pragma unroll
+            for (int j = 0; j < P1K_GB; j++) {
+                const f2 l0 = lds_f2(ws, (int)(wd[j] & 0x3FFu));
+                const f2 l1 = lds_f2(ws + P1K_KPAD * 8, (int)((wd[j] >> 10) & 0x3FFu));
+                const f2 l2 = lds_f2(ws + 2 * P1K_KPAD * 8, (int)(wd[j] >> 20));
+                Lg[j] = (l0 + l1) + l2;
             }
-            if (Lg.y > gv1) {
-                gv1 = Lg.y;
-                gu1 = u;
+            const int un = u0 + 64 * P1K_GB < Upad ? u0 + 64 * P1K_GB : u0;  // (last: re-read)
+#pragma unroll
+            for (int j = 0; j < P1K_GB; j++)
+                wd[j] = tups[un + 64 * j + lane64];
+#pragma unroll
+            for (int j = 0; j < P1K_GB; j++) {
+                const int u = u0 + 64 * j + lane64;
+                if (Lg[j].x > gv0) {
+                    gv0 = Lg[j].x;
+                    gu0 = u;
+                }
+                if (Lg[j].y > gv1) {
+                    gv1 = Lg[j].y;
+                    gu1 = u;
+                }
             }
         }
         wave_argmax_to63(gv0, gu0);
@@ -521,19 +626,20 @@ extern "C" int tdoa_diag_fetch_p1k(unsigned long long *host, int n)
 
 // --------------------------------------------------------------- host side
 namespace {
-template <int NW>
+template <int NW, bool DUAL>
 constexpr size_t p1k_lds(int U)
 {
-    return (size_t)NW * P1K_WAVE_LDS + 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4 + (size_t)U * 4;
+    return (size_t)NW * p1k_wave_lds<DUAL>() + 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4 +
+           (size_t)(U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64) * 4;
 }
 
 int g_p1k_waves = -1;  // 0: use the generic kernels (A/B), else NW
 
-template <int NW>
+template <int NW, bool DUAL>
 int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                float e2, hipStream_t st)
 {
-    const size_t lds = p1k_lds<NW>(kp.U);
+    const size_t lds = p1k_lds<NW, DUAL>(kp.U);
     static int c_dev = -1, c_resident = 0;
     static size_t c_lds = 0;
     int dev = 0;
@@ -541,7 +647,7 @@ int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
     if (dev != c_dev || lds != c_lds) {
         int per_cu = 0, cus = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phat1024<NW>, NW * 64, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phat1024<NW, DUAL>, NW * 64, lds);
         c_resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
         c_dev = dev;
         c_lds = lds;
@@ -550,7 +656,7 @@ int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
     const int64_t groups = (B + NF - 1) / NF;
     const int64_t iters = (groups + c_resident - 1) / c_resident;
     const int64_t grid = (groups + iters - 1) / iters;
-    hipLaunchKernelGGL(k_phat1024<NW>, dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames,
+    hipLaunchKernelGGL((k_phat1024<NW, DUAL>), dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames,
                        B, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -562,6 +668,47 @@ int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
 }
 }  // namespace
 
+// LDS table image of k_phat1024 (layout of the kernel's shared memory from twm on)
+void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
+                         const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img)
+{
+    img.clear();
+    if (M != 3 || N != 1024 || K > P1K_KPAD - 1)
+        return;
+    const int Upad = (U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
+    img.resize((size_t)P1K_IMG_FIXED + (size_t)Upad * 4);
+    float *f = (float *)img.data();
+    const float *tw2 = tw + 2 * N;
+    for (int k = 0; k < 32; k++)  // twm [k][r] = W_1024^{r k}
+        for (int r = 0; r < 32; r++) {
+            const int i = (k * r) & (N - 1);
+            f[2 * (32 * k + r)] = tw[2 * i];
+            f[2 * (32 * k + r) + 1] = tw[2 * i + 1];
+        }
+    f += 2 * 1024;
+    for (int k = 0; k < 16; k++)  // tw2 [k][r] = W_2048^{r + 32 k}
+        for (int r = 0; r < 32; r++) {
+            const int b = r + 32 * k;
+            f[2 * (32 * k + r)] = tw2[2 * b];
+            f[2 * (32 * k + r) + 1] = tw2[2 * b + 1];
+        }
+    f += 2 * 512;
+    for (int e = 0; e < 512; e++) {  // (W[2e], W[2e+1]) / 128
+        f[2 * e] = (float)win[2 * e] * (1.0f / 128.0f);
+        f[2 * e + 1] = (float)win[2 * e + 1] * (1.0f / 128.0f);
+    }
+    f += 2 * 512;
+    for (int k = 0; k < 128; k++)
+        f[k] = k < K ? prior[k] : 0.0f;
+    uint32_t *t = (uint32_t *)(f + 128);
+    // tuples as LDS byte offsets into a wave's [p][KPAD] f2 score table, 10 bits
+    // per pair; padding tuple (127, 127, 127) scores -inf
+    for (int e = 0; e < Upad; e++) {
+        const uint32_t wd = e < U ? tuples[e] : 0x007F7F7Fu;
+        t[e] = ((wd & 0xFFu) << 3) | (((wd >> 8) & 0xFFu) << 13) | (((wd >> 16) & 0xFFu) << 23);
+    }
+}
+
 // config-2 shape (M = 3, N = 1024, S <= 63) with a tuple table that fits the tail
 bool tdoa_phat1024_fits(const tdoa_kparams &kp)
 {
@@ -571,13 +718,13 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp)
         if (g_p1k_waves != 0 && g_p1k_waves != 4 && g_p1k_waves != 8)
             g_p1k_waves = 8;
     }
-    if (g_p1k_waves == 0 || kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1)
+    if (g_p1k_waves == 0 || kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1 || !kp.p1k_img)
         return false;
     // grid scores of a wave's two frames live in its tiles: [3][KPAD] f2 = 3 KiB
-    static_assert(3 * P1K_KPAD * 8 <= P1K_WAVE_LDS, "grid scores exceed the wave's tiles");
+    static_assert(3 * P1K_KPAD * 8 <= p1k_wave_lds<false>(), "grid scores exceed the wave's tiles");
     if (g_p1k_waves == 8)
-        return p1k_lds<8>(kp.U) <= 160 * 1024;
-    return p1k_lds<4>(kp.U) <= 160 * 1024;
+        return p1k_lds<8, false>(kp.U) <= 160 * 1024;
+    return p1k_lds<4, true>(kp.U) <= 160 * 1024;
 }
 
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
@@ -589,6 +736,6 @@ int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (!(e2 >= 1e-30f))
         e2 = 1e-30f;
     hipStream_t st = (hipStream_t)stream;
-    return g_p1k_waves == 4 ? launch_p1k<4>(kp, out, frames, B, e2, st)
-                            : launch_p1k<8>(kp, out, frames, B, e2, st);
+    return g_p1k_waves == 4 ? launch_p1k<4, true>(kp, out, frames, B, e2, st)
+                            : launch_p1k<8, false>(kp, out, frames, B, e2, st);
 }

@@ -15,5 +15,6 @@ bench() {  # name, env...
   tail -1 gpurun_out/p1k_bench_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n value %.4g kernel_ms %.4f frac %.4f' % (d['value'], d['roofline']['kernel_ms'], d['roofline']['frac']))"
 }
 bench new TDOA_PHAT1024_WAVES=$W
-bench ilp TDOA_PHAT1024_WAVES=$W TDOA_LIB=$GRAFT_REPO_ROOT/audio-triangulation_amd/tdoa/libtdoa_ilp.so
+
+
 bench old TDOA_PHAT1024_WAVES=0
