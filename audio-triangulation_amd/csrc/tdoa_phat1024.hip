@@ -164,6 +164,29 @@ __device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16]
 
 // first half of a 32 x 32 FFT_1024 on a residue column: DFT-32 in registers,
 // twiddle W_1024^{-+res k}, column write into the tile
+// ... with the twiddles read from LDS in groups of 8 ahead of their writes
+// (register-lean form for two waves per SIMD)
+template <bool INV, bool HALF_ZERO>
+__device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *tile)
+{
+    fft32p<INV, HALF_ZERO>(v);
+    const int wo = 8 * L.res;
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 8) {
+        f2 tw[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            tw[i] = lds_f2(L.twm, wo + 256 * (k0 + i));
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int k = k0 + i;
+            f2 x = v[brev5(k)];
+            if (k)
+                x = INV ? c_mulconj(x, tw[i]) : c_mul(x, tw[i]);
+            sts_f2(tile, wo + P1K_ROW * k, x);
+        }
+    }
+}
 template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, const f2 (&tw)[32])
 {
@@ -345,7 +368,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
         for (int t = 0; t < 16; t++)
             w[t] = __builtin_nontemporal_load(row + 32 * t);
     };
-    {
+    if constexpr (DUAL) {
         const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
         fetch(n0, f, 0);
         fetch(n1, f, 1);
@@ -374,17 +397,20 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
     for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += (int64_t)gridDim.x * NF) {
         const int64_t f = base + 2 * wave + hw;
         const bool live = f < B;
+        if constexpr (DUAL) {
 #pragma unroll
-        for (int t = 0; t < 16; t++) {
-            w0[t] = n0[t];
-            w1[t] = n1[t];
-            w2[t] = n2[t];
-        }
-        {
+            for (int t = 0; t < 16; t++) {
+                w0[t] = n0[t];
+                w1[t] = n1[t];
+                w2[t] = n2[t];
+            }
             const int64_t fn = f + (int64_t)gridDim.x * NF;
             fetch(n0, fn, 0);
             fetch(n1, fn, 1);
             fetch(n2, fn, 2);
+        } else {  // two waves per SIMD cover the load latency: one mic ahead only
+            fetch(w0, f, 0);
+            fetch(w1, f, 1);
         }
 #ifdef TDOA_DIAG
         ph_acc[15]++;
@@ -477,52 +503,50 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
         } else {
             // one stream: at most three spectra live (U0, U1, V)
             load_win(L, wf);
-            load_twm(L, tw);
             front_end(L, w0, va, wf);
-            fft_col<false, true>(L, va, L.tileA, tw);
+            fetch(w2, f, 2);
+            fft_col_lds<false, true>(L, va, L.tileA);
             fft_row_fwd(L, L.tileA, U0);
             load_tw2(L, t2);
             split_unit(L, U0, e2, t2);
             load_win(L, wf);
-            load_twm(L, tw);
             front_end(L, w1, va, wf);
-            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_col_lds<false, true>(L, va, L.tileA);
             fft_row_fwd(L, L.tileA, U1);
             load_tw2(L, t2);
             split_unit(L, U1, e2, t2);
             P1K_MARK(1);
-            load_twm(L, tw);
 #pragma unroll
             for (int k = 0; k < 33; k++)
                 V[k] = U0[k];
             cross(V, U1);  // pair 0: (0, 1)
+            load_tw2(L, t2);
             pretwiddle(L, V, t2);
             copy32(va, V);
-            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_col_lds<true, false>(L, va, L.tileA);
             fft_row_inv(L, L.tileA, y0, y31);
             finish_pair(0, y0, y31);
             P1K_MARK(2);
             load_win(L, wf);
-            load_twm(L, tw);
             front_end(L, w2, va, wf);
-            fft_col<false, true>(L, va, L.tileA, tw);
+            fft_col_lds<false, true>(L, va, L.tileA);
             fft_row_fwd(L, L.tileA, V);
             load_tw2(L, t2);
             split_unit(L, V, e2, t2);
             cross(U0, V);  // pair 1: (0, 2)
             cross(U1, V);  // pair 2: (1, 2)
             P1K_MARK(3);
-            load_twm(L, tw);
+            load_tw2(L, t2);
             pretwiddle(L, U0, t2);
             copy32(va, U0);
-            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_col_lds<true, false>(L, va, L.tileA);
             fft_row_inv(L, L.tileA, y0, y31);
             finish_pair(1, y0, y31);
             P1K_MARK(4);
-            load_twm(L, tw);
+            load_tw2(L, t2);
             pretwiddle(L, U1, t2);
             copy32(va, U1);
-            fft_col<true, false>(L, va, L.tileA, tw);
+            fft_col_lds<true, false>(L, va, L.tileA);
             fft_row_inv(L, L.tileA, z0, z31);
             finish_pair(2, z0, z31);
         }
@@ -547,50 +571,52 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
         float gv0 = -INFINITY, gv1 = -INFINITY;
         int gu0 = INT_MAX, gu1 = INT_MAX;
         const char *ws = (const char *)wsc;
-        // batches of GB tuples per lane; the next batch's tuple words are read
-        // while the current batch's gathers are in flight
-        uint32_t wd[P1K_GB];
+        // each lane scores 4 consecutive tuples per step (one b128 read of their
+        // words, 12 b64 gathers: within the 15 LDS ops a wave may have in
+        // flight); the next step's words are read while the gathers land.  Per
+        // lane the tuples ascend, so a strict '>' keeps the first maximum.
+        P1K_MARK(7);
+        const uint4 *tq = (const uint4 *)tups;
+        uint4 q = tq[lane64];
+        for (int u0 = 0; u0 < Upad; u0 += 256) {
+            const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
+            f2 Lg[4];
 #pragma unroll
-        for (int j = 0; j < P1K_GB; j++)
-            wd[j] = tups[64 * j + lane64];
-        for (int u0 = 0; u0 < Upad; u0 += 64 * P1K_GB) {
-            f2 Lg[P1K_GB];
-#pragma unroll
-            for (int j = 0; j < P1K_GB; j++) {
-                const f2 l0 = lds_f2(ws, (int)(wd[j] & 0x3FFu));
-                const f2 l1 = lds_f2(ws + P1K_KPAD * 8, (int)((wd[j] >> 10) & 0x3FFu));
-                const f2 l2 = lds_f2(ws + 2 * P1K_KPAD * 8, (int)(wd[j] >> 20));
-                Lg[j] = (l0 + l1) + l2;
+            for (int i = 0; i < 4; i++) {
+                const f2 l0 = lds_f2(ws, (int)(wq[i] & 0x3FFu));
+                const f2 l1 = lds_f2(ws + P1K_KPAD * 8, (int)((wq[i] >> 10) & 0x3FFu));
+                const f2 l2 = lds_f2(ws + 2 * P1K_KPAD * 8, (int)(wq[i] >> 20));
+                Lg[i] = (l0 + l1) + l2;
             }
-            const int un = u0 + 64 * P1K_GB < Upad ? u0 + 64 * P1K_GB : u0;  // (last: re-read)
+            q = tq[(u0 + 256 < Upad ? u0 + 256 : u0) / 4 + lane64];
 #pragma unroll
-            for (int j = 0; j < P1K_GB; j++)
-                wd[j] = tups[un + 64 * j + lane64];
-#pragma unroll
-            for (int j = 0; j < P1K_GB; j++) {
-                const int u = u0 + 64 * j + lane64;
-                if (Lg[j].x > gv0) {
-                    gv0 = Lg[j].x;
+            for (int i = 0; i < 4; i++) {
+                const int u = u0 + 4 * lane64 + i;
+                if (Lg[i].x > gv0) {
+                    gv0 = Lg[i].x;
                     gu0 = u;
                 }
-                if (Lg[j].y > gv1) {
-                    gv1 = Lg[j].y;
+                if (Lg[i].y > gv1) {
+                    gv1 = Lg[i].y;
                     gu1 = u;
                 }
             }
         }
+        P1K_MARK(8);
         wave_argmax_to63(gv0, gu0);
         wave_argmax_to63(gv1, gu1);
+        P1K_MARK(9);
         if (lane64 == 63) {
+            // every L compared false (NaN scores): tuple 0
+            const int ui0 = (gu0 < 0 || gu0 >= kp.U) ? 0 : gu0;
+            const int ui1 = (gu1 < 0 || gu1 >= kp.U) ? 0 : gu1;
+            const int cells[2] = {kp.tuple_cell[ui0], kp.tuple_cell[ui1]};  // both loads first
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int64_t fs = base + 2 * wave + h;
-                int ui = h ? gu1 : gu0;
                 const float v = h ? gv1 : gv0;
+                const int cell = cells[h];
                 if (fs < B) {
-                    if (ui < 0 || ui >= kp.U)  // every L compared false (NaN scores)
-                        ui = 0;
-                    const int cell = kp.tuple_cell[ui];
                     if (out.cell)
                         out.cell[fs] = cell;
                     if (out.max_Lf)

@@ -150,3 +150,33 @@ def test_split_path_chunking_matches_one_chunk():
     for k in ("lags", "gate", "cell", "xy", "max_Lf"):
         assert (big[k][1020:1030] == part[k]).all(), k
     loc.close()
+
+
+def _grid_f32(weighted, lut):
+    """vga_heatmap.h:99-108 on the engine's own float weighted scores, in float32
+    with the kernel's association ((w0 + w1) + w2): max L and the first cell."""
+    w = np.asarray(weighted, np.float32)
+    lut2 = np.asarray(lut).reshape(w.shape[1], -1).astype(np.int64)
+    L = w[:, 0][:, lut2[0]]
+    for p in range(1, w.shape[1]):
+        L = (L + w[:, p][:, lut2[p]]).astype(np.float32)
+    return L.argmax(-1).astype(np.int32), L.max(-1)
+
+
+@pytest.mark.parametrize("kind", ["adc", "full_range", "noise_only"])
+def test_grid_exact_on_own_scores(phat3, kind):
+    """The config-2 kernel prunes the 2469 lag tuples by exact bounds; its cell and
+    max L must equal the exhaustive float32 scan of its own weighted scores bit
+    for bit (ties to the first row-major cell)."""
+    lut = phat3.lut()
+    if kind == "adc":
+        fr, _, _ = synth.adc_frames(2048, 3, 1024, lut.reshape(3, 101, 101), 46, 77, device="cuda")
+    elif kind == "full_range":
+        fr = synth.full_range_frames(512, 3, 1024, 0x51, device="cuda")
+    else:  # uncorrelated mics: flat, noisy scores, weak bounds
+        g = torch.Generator(device="cpu").manual_seed(5)
+        fr = (torch.randint(0, 256, (512, 3, 1024), generator=g, dtype=torch.int16)).cuda()
+    got = _np(phat3.localize(fr, scores=True))
+    cell, mx = _grid_f32(got["weighted_f"], lut)
+    assert (got["cell"] == cell).all()
+    assert (got["max_Lf"] == mx).all()
