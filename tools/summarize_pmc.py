@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KERNELS = {"gcc_phat": "k_gcc_phat", "direct": "k_direct"}
+KERNELS = {"gcc_phat": "k_phat1024", "direct": "k_direct"}
 
 
 def per_dispatch(path, counter, kname):
