@@ -40,49 +40,49 @@ TDOA_PK(c_conj_add_mi, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0
 __device__ __forceinline__ f2 c_mul(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "v"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "v"(w));
     return r;
 }
 // a * conj(w)
 __device__ __forceinline__ f2 c_mulconj(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
-        : "=v"(r)
-        : "v"(a), "v"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "v"(w));
     return r;
 }
 // conj(a) * b
 __device__ __forceinline__ f2 c_conjmul(f2 a, f2 b)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "v"(b), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "v"(b));
     return r;
 }
 // the same with the twiddle in an SGPR pair (compile-time constants)
 __device__ __forceinline__ f2 c_mul_s(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "s"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "s"(w));
     return r;
 }
 __device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
-        : "=v"(r)
-        : "v"(a), "s"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "s"(w));
     return r;
 }
 
@@ -90,19 +90,19 @@ __device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w)
 __device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-        : "=v"(r)
-        : "v"(a), "s"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "s"(w));
     return r;
 }
 __device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w)
 {
     f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,1]"
-        : "=v"(r)
-        : "v"(a), "s"(w), "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,1]"
+        : "=v"(r), "=&v"(t)
+        : "v"(a), "s"(w));
     return r;
 }
 // -i x = (x.y, -x.x);  i x = (-x.y, x.x)
@@ -123,8 +123,10 @@ __device__ __forceinline__ f2 c_i(f2 x)
 __device__ __forceinline__ f2 c_unit(f2 x, float e2)
 {
     f2 t, s;
-    asm("v_pk_mul_f32 %0, %1, %1" : "=v"(t) : "v"(x));
-    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(s) : "v"(t));
+    asm("v_pk_mul_f32 %1, %2, %2\n\t"
+        "v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]"
+        : "=v"(s), "=&v"(t)
+        : "v"(x));
     const float r = __builtin_amdgcn_rsqf(fmaxf(s.x, e2));
     f2 y;
     asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(f2{r, r}));

@@ -12,8 +12,8 @@
 //   z[n] = x[2n] + i x[2n+1]  (n < 512; the upper half is the zero padding)
 //   Z = FFT_1024(z) as 32 x 32: DFT-32 over n1 in registers (lane = residue
 //       column n2 = res(lane)), twiddle W_1024^{n2 k1}, transpose through a
-//       private padded LDS tile (row stride 264 B: b64 writes and reads are
-//       bank-conflict free with no swizzle), DFT-32 over n2.
+//       private padded LDS tile (row stride 264 B, residues 16 and 24 in
+//       swapped slots: b64 writes and reads bank-conflict free), DFT-32 over n2.
 //       Lane l then holds Z[res + 32 k2], k2 = 0..31.
 //   Real-FFT split X[b] (b <-> N - b): lanes l, l^1 hold the partner residues
 //       res, 32 - res; they swap their upper 16 registers by DPP so that the
@@ -30,9 +30,9 @@
 //   swap back to residue columns, y = IFFT_1024(Y) pruned to the outputs
 //   n = n1 (+992) that hold lags -S..S, argmax + lag prior (correlations.c:20-33
 //   semantics on float scores), gate (sample_compute.h:124-134).
-// Per wave and iteration: the grid solve of vga_heatmap.h:99-108 for its two
-// frames at once (lanes split the distinct lag tuples, one b64 gather per pair
-// reads both frames' weighted scores).
+// Per wave and two iterations: the grid solve of vga_heatmap.h:99-108 for its
+// four frames at once (lanes split the distinct lag tuples, one b128 gather per
+// pair reads the four frames' weighted scores).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -55,6 +55,13 @@ constexpr int p1k_wave_lds() { return (DUAL ? 4 : 2) * P1K_TILE; }  // tiles per
 constexpr int P1K_GB = 8;                 // grid tuples per lane per batch
 // LDS table image: twm [32][32] f2 | tw2 [16][32] f2 | win [512] f2 | prior [128] | tuples
 constexpr int P1K_IMG_FIXED = 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4;
+
+// Tile row / column and table column of residue (or DFT index) x: 16 and 24
+// swap places, so the residues of every 16-lane group of a half-wave --
+// {0, 16, 1, 31, .., 7, 25} and {8, 24, 9, 23, .., 15, 17} -- fall on distinct
+// 8-B bank slots mod 16: the transposes' ds_write_b64 / ds_read2_b64 and the
+// table reads (bank = dword mod 32) are conflict-free (plain order: 2-way).
+__host__ __device__ constexpr int slot(int x) { return x == 16 ? 24 : (x == 24 ? 16 : x); }
 
 // residue column held by lane l of a half-wave: lanes (2j, 2j+1) hold the
 // partner residues (j, 32 - j); lanes 0, 1 the self-paired residues 0, 16
@@ -110,6 +117,7 @@ struct Lane {
     int hw;           // half-wave of the wave
     int lane;         // 0..31 within the half-wave
     int res;          // residue column
+    int cs;           // its tile / table slot, slot(res)
     bool is0, is1;    // the self-paired lanes
     char *tileA;      // this half-wave's two transpose tiles
     char *tileB;
@@ -124,19 +132,19 @@ __device__ __forceinline__ void load_twm(const Lane &L, f2 (&tw)[32])  // W_1024
 {
 #pragma unroll
     for (int k = 1; k < 32; k++)
-        tw[k] = lds_f2(L.twm, 8 * L.res + 256 * k);
+        tw[k] = lds_f2(L.twm, 8 * L.cs + 256 * k);
 }
 __device__ __forceinline__ void load_tw2(const Lane &L, f2 (&t2)[16])  // W_2048^{res + 32 k}
 {
 #pragma unroll
     for (int k = 0; k < 16; k++)
-        t2[k] = lds_f2(L.tw2, 8 * L.res + 256 * k);
+        t2[k] = lds_f2(L.tw2, 8 * L.cs + 256 * k);
 }
 __device__ __forceinline__ void load_win(const Lane &L, f2 (&wf)[16])  // W / 128 of words res + 32 t
 {
 #pragma unroll
     for (int t = 0; t < 16; t++)
-        wf[t] = lds_f2(L.win, 8 * L.res + 256 * t);
+        wf[t] = lds_f2(L.win, 8 * L.cs + 256 * t);
 }
 
 // integer front end of one mic row (16 words per lane) -> v[t] = z[res + 32 t]
@@ -170,7 +178,7 @@ template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *tile)
 {
     fft32p<INV, HALF_ZERO>(v);
-    const int wo = 8 * L.res;
+    const int wo = 8 * L.cs;
 #pragma unroll
     for (int k0 = 0; k0 < 32; k0 += 8) {
         f2 tw[8];
@@ -183,7 +191,7 @@ __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *ti
             f2 x = v[brev5(k)];
             if (k)
                 x = INV ? c_mulconj(x, tw[i]) : c_mul(x, tw[i]);
-            sts_f2(tile, wo + P1K_ROW * k, x);
+            sts_f2(tile, wo + P1K_ROW * slot(k), x);
         }
     }
 }
@@ -191,23 +199,23 @@ template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, const f2 (&tw)[32])
 {
     fft32p<INV, HALF_ZERO>(v);
-    const int wo = 8 * L.res;
+    const int wo = 8 * L.cs;
 #pragma unroll
     for (int k = 0; k < 32; k++) {
         f2 x = v[brev5(k)];
         if (k)
             x = INV ? c_mulconj(x, tw[k]) : c_mul(x, tw[k]);
-        sts_f2(tile, wo + P1K_ROW * k, x);
+        sts_f2(tile, wo + P1K_ROW * slot(k), x);
     }
 }
 // second half: row read (row res) + forward DFT-32 -> V[k2] = Z[res + 32 k2]
 __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 (&V)[33])
 {
     f2 v[32];
-    const int ro = P1K_ROW * L.res;
+    const int ro = P1K_ROW * L.cs;
 #pragma unroll
     for (int n = 0; n < 32; n++)
-        v[n] = lds_f2(tile, ro + 8 * n);
+        v[n] = lds_f2(tile, ro + 8 * slot(n));
     fft32p<false, false>(v);
 #pragma unroll
     for (int k = 0; k < 32; k++)
@@ -217,10 +225,10 @@ __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 
 __device__ __forceinline__ void fft_row_inv(const Lane &L, const char *tile, f2 &y0, f2 &y31)
 {
     f2 v[32];
-    const int ro = P1K_ROW * L.res;
+    const int ro = P1K_ROW * L.cs;
 #pragma unroll
     for (int n = 0; n < 32; n++)
-        v[n] = lds_f2(tile, ro + 8 * n);
+        v[n] = lds_f2(tile, ro + 8 * slot(n));
     // outputs n2 = 0 and 31 of the second DFT-32: y0 = sum v[r],
     // y31 = sum v[r] W_32^r = sum_{r<16} (v[r] - v[r+16]) W_32^r
     f2 a[16], d[16];
@@ -339,6 +347,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
     L.hw = hw;
     L.lane = tid & 31;
     L.res = lane_res(L.lane);
+    L.cs = slot(L.res);
     L.is0 = L.lane == 0;
     L.is1 = L.lane == 1;
     char *wtiles = tiles + wave * WAVE_LDS;
@@ -394,7 +403,12 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
     const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
     const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
 
-    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += (int64_t)gridDim.x * NF) {
+    // weighted scores of the previous iteration's frames, held for a grid pass
+    // over four frames (two iterations) at once
+    float pv[3][4];
+    int64_t pbase = -1;
+    const int64_t stride = (int64_t)gridDim.x * NF;
+    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += stride) {
         const int64_t f = base + 2 * wave + hw;
         const bool live = f < B;
         if constexpr (DUAL) {
@@ -556,67 +570,86 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
 
         if (!do_grid)
             continue;
-        // ---- grid solve of this wave's two frames (vga_heatmap.h:99-108): weighted
-        // scores -> [p][k] (frame of half-wave 0, frame of half-wave 1) in the wave's
-        // tile space, lanes split the tuples, (max L, first tuple) per frame
-        float *wsc = (float *)wtiles;  // [P][KPAD][2]
+        // ---- grid solve (vga_heatmap.h:99-108) once per two iterations: the
+        // weighted scores of this wave's four frames (previous iteration: slots
+        // 0, 1; this one: slots 2, 3) -> [p][k][4] in the wave's tile space, so
+        // one b128 gather per pair reads all four; lanes split the tuples and
+        // keep (max L, first tuple) per frame.  An unpaired iteration (the last
+        // of an odd count) fills slots 0, 1 with its own frames.
+        if (pbase < 0 && base + stride < B) {
+#pragma unroll
+            for (int p = 0; p < P; p++)
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    pv[p][c] = wv[p][c];
+            pbase = base;
+            continue;
+        }
+        const bool paired = pbase >= 0;
+        float *wsc = (float *)wtiles;  // [P][KPAD][4]
 #pragma unroll
         for (int p = 0; p < P; p++)
 #pragma unroll
             for (int c = 0; c < 4; c++)
-                if (ok[c])
-                    wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
+                if (ok[c]) {
+                    float *d = wsc + (p * P1K_KPAD + ck[c]) * 4;
+                    d[hw] = paired ? pv[p][c] : wv[p][c];
+                    d[2 + hw] = wv[p][c];
+                }
         if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
-            wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
-        float gv0 = -INFINITY, gv1 = -INFINITY;
-        int gu0 = INT_MAX, gu1 = INT_MAX;
+            *(float4 *)(wsc + (L.lane * P1K_KPAD + P1K_KPAD - 1) * 4) =
+                float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        float gv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int gu[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
         const char *ws = (const char *)wsc;
         // each lane scores 4 consecutive tuples per step (one b128 read of their
-        // words, 12 b64 gathers: within the 15 LDS ops a wave may have in
-        // flight); the next step's words are read while the gathers land.  Per
-        // lane the tuples ascend, so a strict '>' keeps the first maximum.
+        // words, 12 b128 gathers: within the 15 LDS operations a wave may have
+        // in flight); the next step's words are read while the gathers land.
+        // Per lane the tuples ascend, so a strict '>' keeps the first maximum.
         P1K_MARK(7);
         const uint4 *tq = (const uint4 *)tups;
         uint4 q = tq[lane64];
         for (int u0 = 0; u0 < Upad; u0 += 256) {
             const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
-            f2 Lg[4];
+            float4 Lg[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const f2 l0 = lds_f2(ws, (int)(wq[i] & 0x3FFu));
-                const f2 l1 = lds_f2(ws + P1K_KPAD * 8, (int)((wq[i] >> 10) & 0x3FFu));
-                const f2 l2 = lds_f2(ws + 2 * P1K_KPAD * 8, (int)(wq[i] >> 20));
+                // tuple fields are byte offsets of f2 slots: x2 for float4 slots
+                const float4 l0 = *(const float4 *)(ws + 2 * (int)(wq[i] & 0x3FFu));
+                const float4 l1 = *(const float4 *)(ws + P1K_KPAD * 16 + 2 * (int)((wq[i] >> 10) & 0x3FFu));
+                const float4 l2 = *(const float4 *)(ws + 2 * P1K_KPAD * 16 + 2 * (int)(wq[i] >> 20));
                 Lg[i] = (l0 + l1) + l2;
             }
             q = tq[(u0 + 256 < Upad ? u0 + 256 : u0) / 4 + lane64];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int u = u0 + 4 * lane64 + i;
-                if (Lg[i].x > gv0) {
-                    gv0 = Lg[i].x;
-                    gu0 = u;
-                }
-                if (Lg[i].y > gv1) {
-                    gv1 = Lg[i].y;
-                    gu1 = u;
-                }
+                const float lv[4] = {Lg[i].x, Lg[i].y, Lg[i].z, Lg[i].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (lv[j] > gv[j]) {
+                        gv[j] = lv[j];
+                        gu[j] = u;
+                    }
             }
         }
         P1K_MARK(8);
-        wave_argmax_to63(gv0, gu0);
-        wave_argmax_to63(gv1, gu1);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            wave_argmax_to63(gv[j], gu[j]);
         P1K_MARK(9);
         if (lane64 == 63) {
             // every L compared false (NaN scores): tuple 0
-            const int ui0 = (gu0 < 0 || gu0 >= kp.U) ? 0 : gu0;
-            const int ui1 = (gu1 < 0 || gu1 >= kp.U) ? 0 : gu1;
-            const int cells[2] = {kp.tuple_cell[ui0], kp.tuple_cell[ui1]};  // both loads first
+            int cells[4];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int64_t fs = base + 2 * wave + h;
-                const float v = h ? gv1 : gv0;
-                const int cell = cells[h];
-                if (fs < B) {
+            for (int j = 0; j < 4; j++)  // all loads first
+                cells[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int64_t fs = (j < 2 ? pbase : base) + 2 * wave + (j & 1);
+                const float v = gv[j];
+                const int cell = cells[j];
+                if ((j >= 2 || paired) && fs < B) {
                     if (out.cell)
                         out.cell[fs] = cell;
                     if (out.max_Lf)
@@ -629,6 +662,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
                 }
             }
         }
+        pbase = -1;
         P1K_MARK(6);
     }
 #ifdef TDOA_DIAG
@@ -708,20 +742,21 @@ void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int3
     for (int k = 0; k < 32; k++)  // twm [k][r] = W_1024^{r k}
         for (int r = 0; r < 32; r++) {
             const int i = (k * r) & (N - 1);
-            f[2 * (32 * k + r)] = tw[2 * i];
-            f[2 * (32 * k + r) + 1] = tw[2 * i + 1];
+            f[2 * (32 * k + slot(r))] = tw[2 * i];
+            f[2 * (32 * k + slot(r)) + 1] = tw[2 * i + 1];
         }
     f += 2 * 1024;
     for (int k = 0; k < 16; k++)  // tw2 [k][r] = W_2048^{r + 32 k}
         for (int r = 0; r < 32; r++) {
             const int b = r + 32 * k;
-            f[2 * (32 * k + r)] = tw2[2 * b];
-            f[2 * (32 * k + r) + 1] = tw2[2 * b + 1];
+            f[2 * (32 * k + slot(r))] = tw2[2 * b];
+            f[2 * (32 * k + slot(r)) + 1] = tw2[2 * b + 1];
         }
     f += 2 * 512;
-    for (int e = 0; e < 512; e++) {  // (W[2e], W[2e+1]) / 128
-        f[2 * e] = (float)win[2 * e] * (1.0f / 128.0f);
-        f[2 * e + 1] = (float)win[2 * e + 1] * (1.0f / 128.0f);
+    for (int e = 0; e < 512; e++) {  // (W[2e], W[2e+1]) / 128, word e = 32 t + r at slot(r)
+        const int d = (e & ~31) + slot(e & 31);
+        f[2 * d] = (float)win[2 * e] * (1.0f / 128.0f);
+        f[2 * d + 1] = (float)win[2 * e + 1] * (1.0f / 128.0f);
     }
     f += 2 * 512;
     for (int k = 0; k < 128; k++)
@@ -746,8 +781,8 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp)
     }
     if (g_p1k_waves == 0 || kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1 || !kp.p1k_img)
         return false;
-    // grid scores of a wave's two frames live in its tiles: [3][KPAD] f2 = 3 KiB
-    static_assert(3 * P1K_KPAD * 8 <= p1k_wave_lds<false>(), "grid scores exceed the wave's tiles");
+    // grid scores of a wave's four frames live in its tiles: [3][KPAD] float4 = 6 KiB
+    static_assert(3 * P1K_KPAD * 16 <= p1k_wave_lds<false>(), "grid scores exceed the wave's tiles");
     if (g_p1k_waves == 8)
         return p1k_lds<8, false>(kp.U) <= 160 * 1024;
     return p1k_lds<4, true>(kp.U) <= 160 * 1024;

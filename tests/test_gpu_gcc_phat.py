@@ -163,14 +163,17 @@ def _grid_f32(weighted, lut):
     return L.argmax(-1).astype(np.int32), L.max(-1)
 
 
-@pytest.mark.parametrize("kind", ["adc", "full_range", "noise_only"])
+@pytest.mark.parametrize("kind", ["adc", "adc_3iter", "adc_ragged", "full_range", "noise_only"])
 def test_grid_exact_on_own_scores(phat3, kind):
-    """The config-2 kernel prunes the 2469 lag tuples by exact bounds; its cell and
-    max L must equal the exhaustive float32 scan of its own weighted scores bit
-    for bit (ties to the first row-major cell)."""
+    """The config-2 kernel scans the 2469 distinct lag tuples once per two
+    iterations for a wave's four frames; its cell and max L must equal the
+    exhaustive float32 scan of its own weighted scores bit for bit (ties to the
+    first row-major cell).  6144 frames give every wave three iterations (one
+    paired grid pass, one single); 6151 leave a ragged last workgroup."""
     lut = phat3.lut()
-    if kind == "adc":
-        fr, _, _ = synth.adc_frames(2048, 3, 1024, lut.reshape(3, 101, 101), 46, 77, device="cuda")
+    if kind.startswith("adc"):
+        B = {"adc": 2048, "adc_3iter": 6144, "adc_ragged": 6151}[kind]
+        fr, _, _ = synth.adc_frames(B, 3, 1024, lut.reshape(3, 101, 101), 46, 77, device="cuda")
     elif kind == "full_range":
         fr = synth.full_range_frames(512, 3, 1024, 0x51, device="cuda")
     else:  # uncorrelated mics: flat, noisy scores, weak bounds
