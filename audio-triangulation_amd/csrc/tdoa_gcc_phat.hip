@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include "tdoa_device.h"
 #include "tdoa_fft32.h"
@@ -664,6 +665,10 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp);
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
                          int64_t B, float phat_eps, void *stream);
 
+bool tdoa_phat_r16_fits(int M, int N, int S);
+int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+                         float phat_eps, void *scratch, size_t scratch_bytes, void *stream);
+
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp)
 {
     if (tdoa_phat1024_fits(kp))
@@ -686,6 +691,14 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
     if (tdoa_phat1024_fits(kp))
         return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
+    // frame_len 2048 / 4096 with M > 3 or N > 2048: register-pass kernels
+    // (tdoa_phat_r16.hip); TDOA_PHAT_R16=0 keeps the LDS Stockham pair (A/B)
+    static const int use_r16 = [] {
+        const char *s = getenv("TDOA_PHAT_R16");
+        return s ? atoi(s) : 1;
+    }();
+    if (tdoa_gcc_phat_needs_split(kp.M, kp.N) && use_r16 && tdoa_phat_r16_fits(kp.M, kp.N, kp.S))
+        return tdoa_launch_phat_r16(kp, out, frames, B, phat_eps, spec_scratch, spec_bytes, stream);
     if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
         return tdoa_launch_gcc_phat_split(kp, out, frames, B,
                                           eps2 * 1152921504606846976.0f /* 2^60: int16 units */,

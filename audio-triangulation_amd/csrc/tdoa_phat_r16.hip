@@ -1,0 +1,427 @@
+// tdoa_phat_r16.hip -- GCC-PHAT for the long-frame shapes (frame_len 2048 or
+// 4096, any M <= 8: BASELINE configs 3 and 4), two passes per chunk of frames
+// through a unit-spectrum scratch sized to stay in the Infinity Cache:
+//
+//   k_spec16<C>  one workgroup of T = C/16 threads per (frame, mic) row:
+//                integer front end (rolling_buffer.c:64-66 floor-mean DC,
+//                buffer.c:13-16 low byte, buffer.c:4-11 Q15 window) on the
+//                packed samples z[n] = x[2n] + i x[2n+1], a C-point complex
+//                FFT as three register passes (radix C/256, 16, 16; Stockham
+//                order through one padded LDS buffer), the real-FFT split to
+//                X[0..C] of the 2C-point real transform, and the per-mic PHAT
+//                factor U = X / max(|X|, sqrt(eps)), stored as C + 1 bins.
+//   k_pair16<C>  one workgroup per (frame, pair): R = conj(U_i) U_j is already
+//                the unit cross spectrum; the inverse pre-twiddle packs it
+//                into C bins whose inverse C-point FFT holds the correlation
+//                at even / odd lags in its real / imaginary parts.  Only lags
+//                -S..S (S <= 63) are needed, so the inverse is pruned: pass 1
+//                in full, pass 2 computes 4 of its 16 outputs, pass 3 one
+//                output for 64 of its C/R1 columns.  Then the first argmax and
+//                the lag prior (correlations.c:20-33 semantics on float scores).
+//
+// Thread j of a row holds bins j + T q (q < 16) after the forward transform
+// and the same bins of Y before the inverse, so neither end needs a transpose;
+// the partner bin C - b of the split and of the pre-twiddle is read from LDS /
+// the scratch.  LDS index i is padded to i + i/16 (conflict-free b64 access for
+// every pass's stride).  Same definition as oracle/gcc_phat_oracle.py; the PHAT
+// factorisation equals its R / max(|R|, eps) whenever |X_i|, |X_j| >= sqrt(eps).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+#include <cstdio>
+
+#include "tdoa_cplx.h"
+#include "tdoa_internal.h"
+
+int tdoa_set_error(int code, const char *msg);
+
+namespace {
+
+typedef short v2s_r16 __attribute__((ext_vector_type(2)));
+
+// scratch row stride in complex bins: U[0..C] plus padding to 256 B
+template <int C>
+constexpr int r16_row() { return C + 32; }
+
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+__device__ __forceinline__ f2 lds2(const f2 *buf, int i) { return buf[pidx(i)]; }
+__device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
+
+template <int R>
+__device__ constexpr int brev(int k)
+{
+    return R == 16 ? (((k & 1) << 3) | ((k & 2) << 1) | ((k & 4) >> 1) | ((k & 8) >> 3))
+                   : (((k & 1) << 2) | (k & 2) | ((k & 4) >> 2));
+}
+
+// in-place radix-2 DIF DFT-R (R = 8, 16) on the packed primitives: natural-order
+// input, X[k] ends in v[brev<R>(k)].  HZ: inputs R/2..R-1 are zero.  The
+// butterfly twiddle of span s is W_{2s}^j = W_32^{16 j / s}.
+template <int R, bool INV, bool HZ>
+__device__ __forceinline__ void dftp(f2 (&v)[R])
+{
+    constexpr int LOG2R = R == 16 ? 4 : 3;
+#pragma unroll
+    for (int st = 0; st < LOG2R; st++) {  // linear stage index: fully unrolled
+        const int span = R >> (st + 1);
+#pragma unroll
+        for (int start = 0; start < R; start += 2 * span) {
+#pragma unroll
+            for (int j = 0; j < span; j++) {
+                const int k = j * (16 / span);
+                if (HZ && span == R / 2) {
+                    v[j + span] = tw_only<INV>(v[j], k);
+                } else {
+                    const f2 a = v[start + j], b = v[start + j + span];
+                    v[start + j] = a + b;
+                    v[start + j + span] = dif_tw<INV>(a, b, k);
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int block_sum(int s, int *red)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0)
+        red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++)
+        t += red[w];
+    return t;
+}
+
+// ------------------------------------------------------------------ pass 1
+template <int C>
+__global__ void __launch_bounds__(C / 16, 4) k_spec16(tdoa_kparams kp, const int16_t *__restrict__ frames,
+                                                      int64_t row0, f2 *__restrict__ spec, float e2)
+{
+    constexpr int T = C / 16, R1 = C / 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f2 *buf = (f2 *)smem;  // [C + C/16]
+    __shared__ int red[T / 64];
+    const int j = threadIdx.x;
+    const int64_t row = row0 + blockIdx.x;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(frames + row * (int64_t)C);
+    const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
+    const f2 *tw = reinterpret_cast<const f2 *>(kp.tw);
+    const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+
+    // words j + T s (s < 8) = samples 2(j + T s), +1 = z[j + T s]
+    uint32_t w[8], wn[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        w[s] = __builtin_nontemporal_load(x + j + T * s);
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        wn[s] = win[j + T * s];
+    int sum = 0;
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_r16, w[s]), v2s_r16{1, 1}, sum, false);
+    sum = block_sum(sum, red);
+    // floor-mean DC (int64 arithmetic shift == floor); x <<= 8 keeps the low
+    // byte of x - off; ((s << 8) * W) >> 15 == floor(s * W / 128), exact in fp32
+    const uint32_t off = (uint32_t)(sum >> kp.log2N) & 0xFFu;
+    const uint32_t off2 = off | (off << 16);
+    f2 v[16];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const uint32_t d = (w[s] | 0x01000100u) - off2;  // no borrow across the halves
+        const float s0 = (float)(int8_t)(d & 0xFFu), s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+        const float w0 = (float)(int16_t)(wn[s] & 0xFFFFu) * (1.0f / 128.0f);
+        const float w1 = (float)(int16_t)(wn[s] >> 16) * (1.0f / 128.0f);
+        v[s] = f2{floorf(s0 * w0), floorf(s1 * w1)};
+    }
+
+    // Stockham pass 1 (radix R1, Ns = 1): virtual thread j' reads z[j' + 256 r]
+    if constexpr (R1 == 16) {
+#pragma unroll
+        for (int s = 8; s < 16; s++)
+            v[s] = f2{0.0f, 0.0f};
+        dftp<16, false, true>(v);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            sts2(buf, 16 * j + r, v[brev<16>(r)]);
+    } else {  // R1 = 8, T = 128: j' = j (z = v[2r]) and j + 128 (z = v[2r + 1])
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            f2 u[8];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                u[r] = v[2 * r + h];
+#pragma unroll
+            for (int r = 4; r < 8; r++)
+                u[r] = f2{0.0f, 0.0f};
+            dftp<8, false, true>(u);
+            const int jv = j + 128 * h;
+#pragma unroll
+            for (int r = 0; r < 8; r++)
+                sts2(buf, 8 * jv + r, u[brev<8>(r)]);
+        }
+    }
+    __syncthreads();
+
+    // pass 2 (radix 16, Ns = R1): twiddle W_{16 R1}^{r k} = W_C^{16 r k}, k = j mod R1
+    {
+        const int k = j % R1;
+        f2 t[16];
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            t[r] = tw[16 * r * k];
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = lds2(buf, j + T * r);
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            v[r] = c_mul(v[r], t[r]);
+        dftp<16, false, false>(v);
+        __syncthreads();
+        const int o = (j / R1) * 16 * R1 + k;
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            sts2(buf, o + R1 * r, v[brev<16>(r)]);
+    }
+    __syncthreads();
+
+    // pass 3 (radix 16, Ns = T): twiddle W_C^{r j}; outputs Z[j + T r] stay here
+    f2 Z[16];
+    {
+        f2 t[16];
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            t[r] = tw[r * j];
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = lds2(buf, j + T * r);
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            v[r] = c_mul(v[r], t[r]);
+        dftp<16, false, false>(v);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            Z[r] = v[brev<16>(r)];
+    }
+    __syncthreads();
+
+    // real-FFT split (x2): X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), b = j + T q
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+        sts2(buf, j + T * q, Z[q]);
+    __syncthreads();
+    f2 *o = spec + (size_t)blockIdx.x * r16_row<C>();
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int b = j + T * q;
+        const f2 zp = lds2(buf, (C - b) & (C - 1));
+        const f2 e = c_addconj(Z[q], zp);
+        const f2 od = c_mul(c_subconj(Z[q], zp), tw2[b]);
+        o[b] = c_unit(c_add_mi(e, od), e2);
+    }
+    if (j == 0)  // X[C] = 2 (Re Z[0] - Im Z[0]), real
+        o[C] = c_unit(f2{2.0f * (Z[0].x - Z[0].y), 0.0f}, e2);
+}
+
+// ------------------------------------------------------------------ pass 2
+template <int C>
+__global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout out,
+                                                      const f2 *__restrict__ spec, int64_t f_begin,
+                                                      int64_t nblocks)
+{
+    constexpr int T = C / 16, R1 = C / 256, RS = r16_row<C>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f2 *buf = (f2 *)smem;  // [C + C/16]
+    const int j = threadIdx.x, P = kp.P, M = kp.M, K = kp.K, S = kp.S;
+    const f2 *tw = reinterpret_cast<const f2 *>(kp.tw);
+    const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+    // XCD-aware order: each XCD gets a contiguous run of (frame, pair) items,
+    // so the P pairs of a frame read its M unit spectra through one L2
+    int64_t bi = blockIdx.x;
+    if ((nblocks & 7) == 0)
+        bi = (bi & 7) * (nblocks >> 3) + (bi >> 3);
+    const int64_t fl = bi / P;
+    const int p = (int)(bi - fl * P);
+    const f2 *Ui = spec + (size_t)(fl * M + kp.pair_i[p]) * RS;
+    const f2 *Uj = spec + (size_t)(fl * M + kp.pair_j[p]) * RS;
+
+    // Y[b] = (R[b] + R*[C-b]) + i (R[b] - R*[C-b]) conj(W_2C^b), R = conj(U_i) U_j
+    f2 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int b = j + T * q, pb = C - b;  // b = 0 pairs with bin C
+        const f2 Rk = c_conjmul(Ui[b], Uj[b]), Rn = c_conjmul(Ui[pb], Uj[pb]);
+        const f2 s = c_addconj(Rk, Rn);
+        const f2 qq = c_mulconj(c_subconj(Rk, Rn), tw2[b]);
+        v[q] = c_add_i(s, qq);
+    }
+
+    // inverse pass 1 (radix 16, Ns = 1) straight from the registers
+    dftp<16, true, false>(v);
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+        sts2(buf, 16 * j + r, v[brev<16>(r)]);
+    __syncthreads();
+
+    // inverse pass 2 (radix 16, Ns = 16), outputs r'' in {0, 1, 14, 15} only:
+    // the last pass reads columns j' mod 256 in [0, 32) u [224, 256)
+    {
+        const int k = j & 15;
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = lds2(buf, j + T * r);
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            v[r] = c_mulconj(v[r], tw[r * k * R1]);
+        f2 a[8], d[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            a[r] = v[r] + v[r + 8];
+            d[r] = dif_tw<true>(v[r], v[r + 8], 2 * r);
+        }
+        // X0 = sum a, X1 = sum d, X14 = sum_{r<4} (a_r - a_{r+4}) W_8^r, X15 likewise on d
+        f2 x0 = a[0], x1 = d[0], x14 = a[0] - a[4], x15 = d[0] - d[4];
+#pragma unroll
+        for (int r = 1; r < 8; r++) {
+            x0 = x0 + a[r];
+            x1 = x1 + d[r];
+        }
+#pragma unroll
+        for (int r = 1; r < 4; r++) {
+            x14 = x14 + dif_tw<false>(a[r], a[r + 4], 4 * r);
+            x15 = x15 + dif_tw<false>(d[r], d[r + 4], 4 * r);
+        }
+        __syncthreads();
+        const int o = (j >> 4) * 256 + k;
+        sts2(buf, o, x0);
+        sts2(buf, o + 16, x1);
+        sts2(buf, o + 16 * 14, x14);
+        sts2(buf, o + 16 * 15, x15);
+    }
+    __syncthreads();
+    if (j >= 64)
+        return;
+
+    // inverse pass 3 (radix R1, Ns = 256), one output per column:
+    //   lane l < 32:  column j' = l, output 0 -> y[l]
+    //   lane l >= 32: column j' = 192 + l, output R1 - 1 -> y[C - m], m = 64 - l
+    const int l = j;
+    const int jc = l < 32 ? l : 192 + l;
+    const int m = 64 - l;
+    f2 y = lds2(buf, jc);
+#pragma unroll
+    for (int r = 1; r < R1; r++) {
+        const f2 u = lds2(buf, jc + 256 * r);
+        y = y + (l < 32 ? c_mulconj(u, tw[r * jc]) : c_mul(u, tw[r * m]));
+    }
+    // y[n] = r[2n] + i r[2n+1]: lags 2n, 2n + 1 with n = l or -m
+    const float invL = 1.0f / (float)(2 * C);
+    const int n = l < 32 ? l : -m;
+    const int ka = 2 * n + S, kb = 2 * n + 1 + S;
+    const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
+    const float sa = y.x * invL, sb = y.y * invL;
+    float bv = -INFINITY;
+    int bk = INT_MAX;
+    if (oka) {
+        bv = sa;
+        bk = ka;
+    }
+    if (okb && (sb > bv || bk == INT_MAX)) {
+        bv = sb;
+        bk = kb;
+    }
+    wave_argmax_to63(bv, bk);  // first maximum: the lowest lag wins ties
+    bk = __builtin_amdgcn_readlane(bk, 63);
+    bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);  // NaN scores: keep the index in range
+    const int64_t fg = f_begin + fl;
+    const size_t gb = (size_t)(fg * P + p) * K;
+    if (oka) {
+        const int dd = ka > bk ? ka - bk : bk - ka;
+        if (out.scores_f)
+            out.scores_f[gb + ka] = sa;
+        if (out.weighted_f)
+            out.weighted_f[gb + ka] = sa * kp.prior[dd];
+    }
+    if (okb) {
+        const int dd = kb > bk ? kb - bk : bk - kb;
+        if (out.scores_f)
+            out.scores_f[gb + kb] = sb;
+        if (out.weighted_f)
+            out.weighted_f[gb + kb] = sb * kp.prior[dd];
+    }
+    if (l == 0)
+        out.lags[fg * P + p] = bk - S;
+}
+
+__global__ void k_r16_gate(const int32_t *__restrict__ lags, uint8_t *__restrict__ gate, int64_t B, int P)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B)
+        return;
+    int tot = 0;
+    for (int p = 0; p < P; p++) {
+        const int b = lags[f * P + p];
+        tot += b * b;
+    }
+    gate[f] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+}
+
+template <int C>
+int launch_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+               float e2, void *scratch, size_t scratch_bytes, hipStream_t st)
+{
+    const int M = kp.M, P = kp.P;
+    const size_t per_frame = (size_t)M * r16_row<C>() * sizeof(f2);
+    const int64_t chunk = (int64_t)(scratch_bytes / per_frame);
+    if (chunk < 1)
+        return tdoa_set_error(-1, "GCC_PHAT: spectrum scratch smaller than one frame");
+    const size_t lds = (size_t)(C + C / 16) * sizeof(f2);
+    for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+        const int64_t nf = (B - c0) < chunk ? (B - c0) : chunk;
+        if (nf * P > INT_MAX)
+            return tdoa_set_error(-1, "GCC_PHAT: chunk too large for one launch");
+        hipLaunchKernelGGL(k_spec16<C>, dim3((unsigned)(nf * M)), dim3(C / 16), lds, st, kp, frames, c0 * M,
+                           (f2 *)scratch, e2);
+        hipLaunchKernelGGL(k_pair16<C>, dim3((unsigned)(nf * P)), dim3(C / 16), lds, st, kp, out,
+                           (const f2 *)scratch, c0, nf * P);
+    }
+    if (out.gate) {
+        const int64_t g = (B + 255) / 256;
+        hipLaunchKernelGGL(k_r16_gate, dim3((unsigned)g), dim3(256), 0, st, out.lags, out.gate, B, P);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "GCC_PHAT r16 launch: %s", hipGetErrorString(e));
+        return tdoa_set_error(-2, msg);
+    }
+    return 0;
+}
+
+}  // namespace
+
+bool tdoa_phat_r16_fits(int M, int N, int S)
+{
+    return (N == 2048 || N == 4096) && M >= 2 && M <= TDOA_MAX_MICS_K && S <= 63;
+}
+
+int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+                         float phat_eps, void *scratch, size_t scratch_bytes, void *stream)
+{
+    if (!tdoa_phat_r16_fits(kp.M, kp.N, kp.S))
+        return tdoa_set_error(-1, "GCC_PHAT r16: unsupported shape");
+    if (!scratch)
+        return tdoa_set_error(-1, "GCC_PHAT: context has no spectrum scratch");
+    // per-mic clamp |X_m| >= sqrt(eps) in the oracle's units (x / 2^15, X / 2):
+    // |X|^2 >= eps * 2^32 in the kernel's int16 units with the split's factor 2
+    float e2 = phat_eps * 4294967296.0f;
+    if (!(e2 >= 1e-30f))
+        e2 = 1e-30f;
+    hipStream_t st = (hipStream_t)stream;
+    return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)
+                        : launch_r16<2048>(kp, out, frames, B, e2, scratch, scratch_bytes, st);
+}
