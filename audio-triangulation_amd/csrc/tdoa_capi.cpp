@@ -506,7 +506,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     }
     {
         // GCC_PHAT twiddles, in double then rounded once
-        std::vector<float> tw(2 * N + 2 * (N + 1));
+        std::vector<float> tw(2 * N + 2 * (N + 1) + 2 * 3 * 256);
         for (int k = 0; k < N; k++) {
             const double a = -2.0 * M_PI * k / N;
             tw[2 * k] = (float)std::cos(a);
@@ -517,6 +517,21 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             tw[2 * N + 2 * k] = (float)std::cos(a);
             tw[2 * N + 2 * k + 1] = (float)std::sin(a);
         }
+        // coalesced twiddle tables of the long-frame kernels (tdoa_phat_r16.hip):
+        // [r][k] W_N^{(N/256) r k}; [r][l] W_N^{r l}; [r][h] W_N^{16 r h}  (r, k, l, h < 16)
+        {
+            float *t = tw.data() + 2 * N + 2 * (N + 1);
+            const int R1 = N >= 256 ? N / 256 : 1;
+            const int mul[3] = {R1, 1, 16};
+            for (int s = 0; s < 3; s++)
+                for (int r = 0; r < 16; r++)
+                    for (int k = 0; k < 16; k++) {
+                        const long e = ((long)mul[s] * r * k) % N;
+                        const double a = -2.0 * M_PI * (double)e / N;
+                        t[2 * (256 * s + 16 * r + k)] = (float)std::cos(a);
+                        t[2 * (256 * s + 16 * r + k) + 1] = (float)std::sin(a);
+                    }
+        }
         if (hipMalloc(&c->d_tw, sizeof(float) * tw.size()) != hipSuccess ||
             hipMemcpy(c->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice) !=
                 hipSuccess) {
@@ -526,6 +541,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         }
         kp.tw = c->d_tw;
         kp.tw2 = c->d_tw + 2 * N;
+        kp.r16_tw = c->d_tw + 2 * N + 2 * (N + 1);
         std::vector<uint8_t> img;
         tdoa_phat1024_image(M, N, c->K, c->U, tw.data(), c->win.data(), c->prior.data(),
                             c->tuples.data(), img);

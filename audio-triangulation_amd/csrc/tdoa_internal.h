@@ -43,6 +43,7 @@ struct tdoa_kparams {
     const int32_t *tuple_cell; // [U] first row-major cell of each tuple
     const float *tw;           // GCC_PHAT: e^{-2 pi i k/N}, k < N   (re, im)
     const float *tw2;          // GCC_PHAT: e^{-2 pi i k/2N}, k <= N (re, im)
+    const float *r16_tw;       // GCC_PHAT long frames: [3][16][16] W_N^{(N/256) r k}, W_N^{r l}, W_N^{16 r h}
     const uint8_t *lut;        // [P][G] lag index per cell (heat map)
     const void *p1k_img;       // config-2 GCC-PHAT kernel: its LDS table image (16-B units)
     int32_t p1k_img_bytes;

@@ -82,6 +82,15 @@ __device__ __forceinline__ void dftp(f2 (&v)[R])
     }
 }
 
+// coalesced twiddles (kp.r16_tw): [0][r][k] W_C^{R1 r k} = W_256^{r k},
+// [1][r][l] W_C^{r l}, [2][r][h] W_C^{16 r h}; W_C^{r x} (x < 256) = [1][r][x&15] [2][r][x>>4]
+__device__ __forceinline__ f2 tw256(const f2 *tt, int r, int k) { return tt[16 * r + k]; }
+__device__ __forceinline__ f2 tw16h(const f2 *tt, int r, int h) { return tt[512 + 16 * r + h]; }
+__device__ __forceinline__ f2 twC(const f2 *tt, int r, int x)
+{
+    return c_mul(tt[256 + 16 * r + (x & 15)], tt[512 + 16 * r + (x >> 4)]);
+}
+
 __device__ __forceinline__ int block_sum(int s, int *red)
 {
 #pragma unroll
@@ -109,8 +118,8 @@ __global__ void __launch_bounds__(C / 16, 4) k_spec16(tdoa_kparams kp, const int
     const int64_t row = row0 + blockIdx.x;
     const uint32_t *x = reinterpret_cast<const uint32_t *>(frames + row * (int64_t)C);
     const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
-    const f2 *tw = reinterpret_cast<const f2 *>(kp.tw);
     const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+    const f2 *tt = reinterpret_cast<const f2 *>(kp.r16_tw);
 
     // words j + T s (s < 8) = samples 2(j + T s), +1 = z[j + T s]
     uint32_t w[8], wn[8];
@@ -173,7 +182,7 @@ __global__ void __launch_bounds__(C / 16, 4) k_spec16(tdoa_kparams kp, const int
         f2 t[16];
 #pragma unroll
         for (int r = 1; r < 16; r++)
-            t[r] = tw[16 * r * k];
+            t[r] = tw16h(tt, r, k);  // W_C^{16 r k}
 #pragma unroll
         for (int r = 0; r < 16; r++)
             v[r] = lds2(buf, j + T * r);
@@ -195,7 +204,7 @@ __global__ void __launch_bounds__(C / 16, 4) k_spec16(tdoa_kparams kp, const int
         f2 t[16];
 #pragma unroll
         for (int r = 1; r < 16; r++)
-            t[r] = tw[r * j];
+            t[r] = twC(tt, r, j);
 #pragma unroll
         for (int r = 0; r < 16; r++)
             v[r] = lds2(buf, j + T * r);
@@ -237,8 +246,8 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *buf = (f2 *)smem;  // [C + C/16]
     const int j = threadIdx.x, P = kp.P, M = kp.M, K = kp.K, S = kp.S;
-    const f2 *tw = reinterpret_cast<const f2 *>(kp.tw);
     const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+    const f2 *tt = reinterpret_cast<const f2 *>(kp.r16_tw);
     // XCD-aware order: each XCD gets a contiguous run of (frame, pair) items,
     // so the P pairs of a frame read its M unit spectra through one L2
     int64_t bi = blockIdx.x;
@@ -249,16 +258,31 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
     const f2 *Ui = spec + (size_t)(fl * M + kp.pair_i[p]) * RS;
     const f2 *Uj = spec + (size_t)(fl * M + kp.pair_j[p]) * RS;
 
-    // Y[b] = (R[b] + R*[C-b]) + i (R[b] - R*[C-b]) conj(W_2C^b), R = conj(U_i) U_j
+    // Y[b] = s + i q with s = R[b] + R*[C-b], q = (R[b] - R*[C-b]) conj(W_2C^b),
+    // R = conj(U_i) U_j; and, from the same four bins, Y[C-b] = conj(s - i q)
+    // (W_2C^{C-b} = -conj(W_2C^b)).  Thread j computes b = j + T r for r < 8 and
+    // the partners C - b, which are the bins r >= 8 of thread T - j (thread 0:
+    // its own, plus the self-paired C/2): one read of every U bin per pair.
     f2 v[16];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int b = j + T * q, pb = C - b;  // b = 0 pairs with bin C
+    for (int r = 0; r < 8; r++) {
+        const int b = j + T * r, pb = C - b;  // b = 0 pairs with bin C
         const f2 Rk = c_conjmul(Ui[b], Uj[b]), Rn = c_conjmul(Ui[pb], Uj[pb]);
         const f2 s = c_addconj(Rk, Rn);
         const f2 qq = c_mulconj(c_subconj(Rk, Rn), tw2[b]);
-        v[q] = c_add_i(s, qq);
+        v[r] = c_add_i(s, qq);
+        if (b != 0)
+            sts2(buf, pb, c_conj_add_mi(s, qq));
     }
+    if (j == 0) {  // Y[C/2] from R[C/2] alone
+        const f2 Rh = c_conjmul(Ui[C / 2], Uj[C / 2]);
+        sts2(buf, C / 2, c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), tw2[C / 2])));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 8; r < 16; r++)
+        v[r] = lds2(buf, j + T * r);
+    __syncthreads();  // the exchange slots are overwritten by pass 1
 
     // inverse pass 1 (radix 16, Ns = 1) straight from the registers
     dftp<16, true, false>(v);
@@ -276,7 +300,7 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
             v[r] = lds2(buf, j + T * r);
 #pragma unroll
         for (int r = 1; r < 16; r++)
-            v[r] = c_mulconj(v[r], tw[r * k * R1]);
+            v[r] = c_mulconj(v[r], tw256(tt, r, k));
         f2 a[8], d[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) {
@@ -316,7 +340,7 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
 #pragma unroll
     for (int r = 1; r < R1; r++) {
         const f2 u = lds2(buf, jc + 256 * r);
-        y = y + (l < 32 ? c_mulconj(u, tw[r * jc]) : c_mul(u, tw[r * m]));
+        y = y + (l < 32 ? c_mulconj(u, twC(tt, r, jc)) : c_mul(u, twC(tt, r, m)));
     }
     // y[n] = r[2n] + i r[2n+1]: lags 2n, 2n + 1 with n = l or -m
     const float invL = 1.0f / (float)(2 * C);
