@@ -186,6 +186,173 @@ __global__ void __launch_bounds__(TPB) k_stream_trigger(tdoa_stream_params sp)
     }
 }
 
+// ------------------------------------------- register trigger scan (N = 2H)
+// One wave per stream, four streams per workgroup, no LDS.  Lane k holds, for
+// rows r = 0, 1, 2, the G = H/64 local samples l = rH + Gk + i (i < G) of every
+// mic: candidate a = Gk + i needs the prefix sums at a, a + N/2 = a + H and
+// a + N = a + 2H, i.e. at position i of the lane's own three chunks.  The chunk
+// totals are wave-scanned (DPP), the rest is a running sum in registers.  Same
+// trigger as k_stream_trigger (sample_compute.h:75-91, rolling_buffer.c:73-85).
+
+// inclusive wave scan (rows by row_shr, then row_bcast:15 / :31)
+__device__ __forceinline__ int wave_scan_incl(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+template <int G, int M>
+__global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp, int64_t S)
+{
+    constexpr int H = 64 * G, N = 2 * H, CB = G * M, CW = (CB + 3) / 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S)
+        return;  // whole wave: no workgroup barrier below
+    const int64_t pos = *sp.pos;       // samples consumed before this hop
+    const int64_t base = pos + 1 - N;  // stream index of local sample 0
+    const int64_t cl = sp.capture_len;
+    const uint8_t *cap = sp.capture + (size_t)s * cl * M;
+    int64_t j0 = base % cl;
+    if (j0 < 0)
+        j0 += cl;
+
+    // x[r][w]: the chunk's CB bytes (sample i, mic m at byte i M + m), packed
+    uint32_t x[3][CW];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int64_t l0 = base + r * H + G * lane;  // stream index of the chunk
+        int64_t j = j0 + r * H + G * lane;
+        if (j >= cl)
+            j -= cl;
+        // contiguous, and the aligned word reads (up to 7 bytes past the chunk)
+        // stay inside this stream's ring
+        if (l0 >= 0 && (j + G) * M + 7 <= cl * M) {
+            const size_t cb = (size_t)j * M;
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(cap + (cb & ~(size_t)3));
+            const uint32_t sh = (uint32_t)(((uintptr_t)cap + cb) & 3u);
+            uint32_t w[CW + 1];
+#pragma unroll
+            for (int k = 0; k <= CW; k++)
+                w[k] = wp[k];
+#pragma unroll
+            for (int k = 0; k < CW; k++)
+                x[r][k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        } else {  // stream start (zeros) or the ring's end
+#pragma unroll
+            for (int k = 0; k < CW; k++)
+                x[r][k] = 0;
+#pragma unroll
+            for (int i = 0; i < G; i++) {
+                int64_t ji = j + i;
+                if (ji >= cl)
+                    ji -= cl;
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    const int b = i * M + m;
+                    const uint32_t v = l0 + i < 0 ? 0u : (uint32_t)cap[(size_t)ji * M + m];
+                    x[r][b >> 2] |= v << (8 * (b & 3));
+                }
+            }
+        }
+    }
+    auto smp = [&](int r, int i, int m) -> int {
+        const int b = i * M + m;
+        return (int)((x[r][b >> 2] >> (8 * (b & 3))) & 0xFFu);
+    };
+    // exclusive prefix at each chunk start: sum x per mic, sum x^2 over mics
+    int q1[3][M], q2[3];
+    {
+        int tot1[M], tot2 = 0;
+#pragma unroll
+        for (int m = 0; m < M; m++)
+            tot1[m] = 0;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            int c2 = 0;
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                int c1 = 0;
+#pragma unroll
+                for (int i = 0; i < G; i++) {
+                    const int v = smp(r, i, m);
+                    c1 += v;
+                    c2 += v * v;
+                }
+                const int inc = wave_scan_incl(c1);
+                q1[r][m] = tot1[m] + inc - c1;
+                tot1[m] += __builtin_amdgcn_readlane(inc, 63);
+            }
+            const int inc2 = wave_scan_incl(c2);
+            q2[r] = tot2 + inc2 - c2;
+            tot2 += __builtin_amdgcn_readlane(inc2, 63);
+        }
+    }
+    // candidates a = G lane + i in ascending order: powers of the older and
+    // newer halves, summed over mics; the first firing one
+    constexpr int hb = __builtin_ctz(N) - 1;
+    const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
+    const int64_t amin = sp.ring_start[s] + N - pos - 1;  // full ring: >= N samples since the last trigger
+    int fi = -1;
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+        const int a = G * lane + i;
+        long long pout = (long long)(q2[1] - q2[0]) << hb, pin = (long long)(q2[2] - q2[1]) << hb;
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const long long so1 = q1[1][m] - q1[0][m], si1 = q1[2][m] - q1[1][m];
+            pout -= so1 * so1;
+            pin -= si1 * si1;
+        }
+        if (fi < 0 && a >= amin && pout > thr + pin)
+            fi = i;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                const int v = smp(r, i, m);
+                q1[r][m] += v;
+                q2[r] += v * v;
+            }
+        }
+    }
+    const uint64_t fire = __ballot(fi >= 0);
+    if (fire == 0)
+        return;
+    const int fl = __builtin_ctzll(fire);  // lowest lane = lowest candidates
+    const int a = G * fl + __builtin_amdgcn_readlane(fi, fl);
+    int slot = 0;
+    if (lane == 0) {
+        slot = atomicAdd(sp.count, 1);
+        const int64_t end = pos + 1 + a;
+        sp.ids[slot] = (int32_t)s;
+        sp.end[slot] = end;
+        sp.ring_start[s] = end;
+    }
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    // the frame: local samples a .. a + N - 1 of every mic (rolling_buffer.c:48-62 order)
+    int16_t *dst = sp.frames + (size_t)slot * M * N;
+    int64_t ja = j0 + a + lane;
+    if (ja >= cl)
+        ja -= cl;
+#pragma unroll 4
+    for (int t = 0; t < N / 64; t++) {
+        const int n = lane + 64 * t;
+        int64_t jn = ja + 64 * t;
+        while (jn >= cl)
+            jn -= cl;
+        const bool neg = base + a + n < 0;
+#pragma unroll
+        for (int m = 0; m < M; m++)
+            dst[(size_t)m * N + n] = neg ? (int16_t)0 : (int16_t)cap[(size_t)jn * M + m];
+    }
+}
+
 // correlations.c:40-43 in the reference's float/double steps
 __device__ __forceinline__ float decay_us(uint64_t now, uint64_t last)
 {
@@ -337,8 +504,38 @@ size_t tdoa_stream_trigger_lds(int M, int N, int H)
     return ((M * L * 2 + 15) & ~(size_t)15) + (((L + 1) * 4 + 15) & ~(size_t)15) + (L + 1) * 8;
 }
 
+template <int G>
+static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+{
+    const dim3 grid((unsigned)((S + 3) / 4));
+    if (sp.M == 2)
+        hipLaunchKernelGGL((k_stream_trigger_w<G, 2>), grid, dim3(256), 0, st, sp, S);
+    else if (sp.M == 3)
+        hipLaunchKernelGGL((k_stream_trigger_w<G, 3>), grid, dim3(256), 0, st, sp, S);
+    else if (sp.M == 4)
+        hipLaunchKernelGGL((k_stream_trigger_w<G, 4>), grid, dim3(256), 0, st, sp, S);
+    else
+        return false;
+    return true;
+}
+
 int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream)
 {
+    // register scan when N = 2H (config 5: N 1024, hop 512), aligned capture
+    if (sp.N == 2 * sp.H && ((uintptr_t)sp.capture & 3) == 0 && sp.capture_len >= (int64_t)sp.N + 2 * sp.H) {
+        hipStream_t st = (hipStream_t)stream;
+        bool ok = false;
+        if (sp.H == 256)
+            ok = launch_trigger_w<4>(sp, S, st);
+        else if (sp.H == 512)
+            ok = launch_trigger_w<8>(sp, S, st);
+        else if (sp.H == 1024)
+            ok = launch_trigger_w<16>(sp, S, st);
+        if (ok) {
+            hipError_t e = hipGetLastError();
+            return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger_w launch");
+        }
+    }
     if (sp.H > TPB * MAX_CAND)
         return tdoa_set_error(-1, "stream: hop too large");
     const size_t lds = tdoa_stream_trigger_lds(sp.M, sp.N, sp.H);
