@@ -370,121 +370,162 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
     __shared__ int redi[TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = TPB / 64;
     const int K = kp.K, P = kp.P;
-    const int slot = blockIdx.x;
     const int cnt = *sp.count;
-    if (slot == 0 && tid == 0) {
-        *sp.pos += sp.H;  // every block of k_stream_trigger has read it
-        sp.stats[0] += cnt;
-        if (out.count)
-            *out.count = cnt;
-    }
-    if (slot >= cnt)
-        return;
-    const int s = sp.ids[slot];
-    if (out.lags) {
-        for (int p = tid; p < P; p += TPB)
-            out.lags[(size_t)slot * P + p] = sp.fresh_lags[(size_t)slot * P + p];
-    }
-    if (tid == 0) {
-        if (out.stream_id)
-            out.stream_id[slot] = s;
-        if (out.end)
-            out.end[slot] = sp.end[slot];
-        if (out.gate)
-            out.gate[slot] = sp.fresh_gate[slot];
-    }
-    if (!sp.fresh_gate[slot]) {  // sample_compute.h:134: only gated frames update
+    if (blockIdx.x == 0) {
+        // gated frames of this hop: block 0 sums the batch's gate bytes (a
+        // per-slot atomic on one counter serialises in L2)
+        int g = 0;
+        for (int i = tid; i < cnt; i += TPB)
+            g += sp.fresh_gate[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+            g += __shfl_xor(g, o, 64);
+        if (lane == 0)
+            redi[wave] = g;
+        __syncthreads();
         if (tid == 0) {
-            if (out.cell)
-                out.cell[slot] = -1;
+            for (int w = 1; w < nwaves; w++)
+                g += redi[w];
+            *sp.pos += sp.H;  // every block of k_stream_trigger has read it
+            sp.stats[0] += cnt;
+            sp.stats[1] += g;
+            if (out.count)
+                *out.count = cnt;
         }
-        return;
     }
-    if (tid == 0)
-        atomicAdd((unsigned long long *)&sp.stats[1], 1ull);
-    const uint64_t now = (uint64_t)sp.end[slot] * 1000000u / (uint64_t)sp.fs;
-    const float dec = decay_us(now, sp.last[s]);
-    int64_t *est = sp.est + (size_t)s * P * K;
-    const int64_t *fr = sp.fresh + (size_t)slot * P * K;
-    for (int p = wave; p < P; p += nwaves) {
+    // persistent over the compact batch (its size is only known on the device)
+    for (int slot = blockIdx.x; slot < cnt; slot += gridDim.x) {
+    __syncthreads();  // the previous slot's W and reductions are consumed
+        const int s = sp.ids[slot];
+        if (out.lags) {
+            for (int p = tid; p < P; p += TPB)
+                out.lags[(size_t)slot * P + p] = sp.fresh_lags[(size_t)slot * P + p];
+        }
+        if (tid == 0) {
+            if (out.stream_id)
+                out.stream_id[slot] = s;
+            if (out.end)
+                out.end[slot] = sp.end[slot];
+            if (out.gate)
+                out.gate[slot] = sp.fresh_gate[slot];
+        }
+        if (!sp.fresh_gate[slot]) {  // sample_compute.h:134: only gated frames update
+            if (tid == 0) {
+                if (out.cell)
+                    out.cell[slot] = -1;
+            }
+            continue;
+        }
+        const uint64_t now = (uint64_t)sp.end[slot] * 1000000u / (uint64_t)sp.fs;
+        const float dec = decay_us(now, sp.last[s]);
+        int64_t *est = sp.est + (size_t)s * P * K;
+        const int64_t *fr = sp.fresh + (size_t)slot * P * K;
+        for (int p = wave; p < P; p += nwaves) {
+            int64_t bv = INT64_MIN;
+            int bk = INT_MAX;
+            for (int k = lane; k < 128; k += 64) {
+                if (k < K) {
+                    const int64_t ev = est[p * K + k];
+                    const float delta = (float)(fr[p * K + k] - ev) * dec;
+                    const float sum = (float)ev + delta;
+                    const int64_t nv = (int64_t)sum;
+                    est[p * K + k] = nv;
+                    W[p * K + k] = nv;
+                    if (nv > bv) {
+                        bv = nv;
+                        bk = k;
+                    }
+                }
+            }
+            for (int m = 32; m >= 1; m >>= 1) {
+                const int64_t ov = __shfl_xor(bv, m, 64);
+                const int ok = __shfl_xor(bk, m, 64);
+                if (ov > bv || (ov == bv && ok < bk)) {
+                    bv = ov;
+                    bk = ok;
+                }
+            }
+            if (lane == 0 && out.ema_best)
+                out.ema_best[(size_t)slot * P + p] = bk - kp.S;
+        }
+        __syncthreads();
+        if (tid == 0)
+            sp.last[s] = now;
+        // grid solve on the EMA scores over the distinct lag tuples
         int64_t bv = INT64_MIN;
-        int bk = INT_MAX;
-        for (int k = lane; k < 128; k += 64) {
-            if (k < K) {
-                const int64_t ev = est[p * K + k];
-                const float delta = (float)(fr[p * K + k] - ev) * dec;
-                const float sum = (float)ev + delta;
-                const int64_t nv = (int64_t)sum;
-                est[p * K + k] = nv;
-                W[p * K + k] = nv;
-                if (nv > bv) {
-                    bv = nv;
-                    bk = k;
+        int bu = INT_MAX;
+        if (kp.TW == 1) {
+            // 3-4 mic grids: a thread's tuple words are loaded 8 at a time ahead of
+            // their gathers (one L2 round trip per 8 tuples, not per tuple)
+            for (int u0 = tid; u0 < kp.U; u0 += 8 * TPB) {
+                uint32_t wd[8];
+    #pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const int u = u0 + t * TPB;
+                    wd[t] = u < kp.U ? kp.tuples[u] : 0u;
+                }
+    #pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const int u = u0 + t * TPB;
+                    if (u < kp.U) {
+                        int64_t Lv = 0;
+                        for (int p = 0; p < P; p++)
+                            Lv += W[p * K + ((wd[t] >> (8 * p)) & 0xFFu)];
+                        if (Lv > bv) {  // ascending u per thread: strict '>' keeps the first
+                            bv = Lv;
+                            bu = u;
+                        }
+                    }
+                }
+            }
+        } else {
+            for (int u = tid; u < kp.U; u += TPB) {
+                int64_t Lv = 0;
+                for (int tw = 0; tw < kp.TW; tw++) {
+                    const uint32_t word = kp.tuples[u * kp.TW + tw];
+                    for (int b = 0; b < 4; b++) {
+                        const int p = 4 * tw + b;
+                        if (p < P)
+                            Lv += W[p * K + ((word >> (8 * b)) & 0xFFu)];
+                    }
+                }
+                if (Lv > bv) {
+                    bv = Lv;
+                    bu = u;
                 }
             }
         }
         for (int m = 32; m >= 1; m >>= 1) {
             const int64_t ov = __shfl_xor(bv, m, 64);
-            const int ok = __shfl_xor(bk, m, 64);
-            if (ov > bv || (ov == bv && ok < bk)) {
+            const int ou = __shfl_xor(bu, m, 64);
+            if (ov > bv || (ov == bv && ou < bu)) {
                 bv = ov;
-                bk = ok;
+                bu = ou;
             }
         }
-        if (lane == 0 && out.ema_best)
-            out.ema_best[(size_t)slot * P + p] = bk - kp.S;
-    }
-    __syncthreads();
-    if (tid == 0)
-        sp.last[s] = now;
-    // grid solve on the EMA scores over the distinct lag tuples
-    int64_t bv = INT64_MIN;
-    int bu = INT_MAX;
-    for (int u = tid; u < kp.U; u += TPB) {
-        int64_t Lv = 0;
-        for (int tw = 0; tw < kp.TW; tw++) {
-            const uint32_t word = kp.tuples[u * kp.TW + tw];
-            for (int b = 0; b < 4; b++) {
-                const int p = 4 * tw + b;
-                if (p < P)
-                    Lv += W[p * K + ((word >> (8 * b)) & 0xFFu)];
+        if (lane == 0) {
+            redv[wave] = bv;
+            redi[wave] = bu;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < nwaves; w++)
+                if (redv[w] > bv || (redv[w] == bv && redi[w] < bu)) {
+                    bv = redv[w];
+                    bu = redi[w];
+                }
+            if (bu < 0 || bu >= kp.U)
+                bu = 0;
+            const int cell = kp.tuple_cell[bu];
+            if (out.cell)
+                out.cell[slot] = cell;
+            if (out.max_L)
+                out.max_L[slot] = bv;
+            if (out.xy) {
+                const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+                out.xy[2 * slot] = (float)(cx - kp.half_w) / kp.grid_scale;
+                out.xy[2 * slot + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
             }
-        }
-        if (Lv > bv) {
-            bv = Lv;
-            bu = u;
-        }
-    }
-    for (int m = 32; m >= 1; m >>= 1) {
-        const int64_t ov = __shfl_xor(bv, m, 64);
-        const int ou = __shfl_xor(bu, m, 64);
-        if (ov > bv || (ov == bv && ou < bu)) {
-            bv = ov;
-            bu = ou;
-        }
-    }
-    if (lane == 0) {
-        redv[wave] = bv;
-        redi[wave] = bu;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < nwaves; w++)
-            if (redv[w] > bv || (redv[w] == bv && redi[w] < bu)) {
-                bv = redv[w];
-                bu = redi[w];
-            }
-        if (bu < 0 || bu >= kp.U)
-            bu = 0;
-        const int cell = kp.tuple_cell[bu];
-        if (out.cell)
-            out.cell[slot] = cell;
-        if (out.max_L)
-            out.max_L[slot] = bv;
-        if (out.xy) {
-            const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
-            out.xy[2 * slot] = (float)(cx - kp.half_w) / kp.grid_scale;
-            out.xy[2 * slot + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
         }
     }
 }
@@ -550,7 +591,8 @@ int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &
                               const tdoa_stream_kout &out, int64_t S, void *stream)
 {
     const size_t lds = (size_t)kp.P * kp.K * 8;
-    hipLaunchKernelGGL(k_stream_update, dim3((unsigned)S), dim3(TPB), lds, (hipStream_t)stream, sp,
+    const int64_t grid = S < 2048 ? S : 2048;  // persistent: up to 8 workgroups per CU
+    hipLaunchKernelGGL(k_stream_update, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(TPB), lds, (hipStream_t)stream, sp,
                        kp, out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail_hip(e, "k_stream_update launch");
