@@ -411,6 +411,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
     for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += stride) {
         const int64_t f = base + 2 * wave + hw;
         const bool live = f < B;
+        const int64_t fn = f + (int64_t)gridDim.x * NF;  // next iteration's frame
         if constexpr (DUAL) {
 #pragma unroll
             for (int t = 0; t < 16; t++) {
@@ -418,10 +419,8 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
                 w1[t] = n1[t];
                 w2[t] = n2[t];
             }
-            const int64_t fn = f + (int64_t)gridDim.x * NF;
-            fetch(n0, fn, 0);
-            fetch(n1, fn, 1);
-            fetch(n2, fn, 2);
+            // the next frame's words are fetched after the register peak of
+            // this iteration (pair (0,1) inverse | mic 2 forward), not here
         } else {  // two waves per SIMD cover the load latency: one mic ahead only
             fetch(w0, f, 0);
             fetch(w1, f, 1);
@@ -496,6 +495,9 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
             fft_row_inv(L, L.tileA, y0, y31);
             fft_row_fwd(L, L.tileB, V);
             finish_pair(0, y0, y31);
+            fetch(n0, fn, 0);
+            fetch(n1, fn, 1);
+            fetch(n2, fn, 2);
             P1K_MARK(3);
             load_tw2(L, t2);
             split_unit(L, V, e2, t2);
