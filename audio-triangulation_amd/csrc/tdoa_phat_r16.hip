@@ -238,13 +238,13 @@ __global__ void __launch_bounds__(C / 16, 4) k_spec16(tdoa_kparams kp, const int
 
 // ------------------------------------------------------------------ pass 2
 template <int C>
-__global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout out,
+__global__ void __launch_bounds__(C / 16, 6) k_pair16(tdoa_kparams kp, tdoa_kout out,
                                                       const f2 *__restrict__ spec, int64_t f_begin,
                                                       int64_t nblocks)
 {
     constexpr int T = C / 16, R1 = C / 256, RS = r16_row<C>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    f2 *buf = (f2 *)smem;  // [C + C/16]
+    f2 *buf = (f2 *)smem;  // [C/2 + C/32]: half of the padded C-point buffer
     const int j = threadIdx.x, P = kp.P, M = kp.M, K = kp.K, S = kp.S;
     const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
     const f2 *tt = reinterpret_cast<const f2 *>(kp.r16_tw);
@@ -272,40 +272,53 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
         const f2 qq = c_mulconj(c_subconj(Rk, Rn), tw2[b]);
         v[r] = c_add_i(s, qq);
         if (b != 0)
-            sts2(buf, pb, c_conj_add_mi(s, qq));
+            sts2(buf, pb - C / 2, c_conj_add_mi(s, qq));  // pb in (C/2, C)
     }
     if (j == 0) {  // Y[C/2] from R[C/2] alone
         const f2 Rh = c_conjmul(Ui[C / 2], Uj[C / 2]);
-        sts2(buf, C / 2, c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), tw2[C / 2])));
+        sts2(buf, 0, c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), tw2[C / 2])));
     }
     __syncthreads();
 #pragma unroll
     for (int r = 8; r < 16; r++)
-        v[r] = lds2(buf, j + T * r);
+        v[r] = lds2(buf, j + T * r - C / 2);
     __syncthreads();  // the exchange slots are overwritten by pass 1
 
-    // inverse pass 1 (radix 16, Ns = 1) straight from the registers
+    // inverse pass 1 (radix 16, Ns = 1) straight from the registers; its
+    // outputs 16 j + r'' go through the half-size buffer in two rounds
+    // (threads j < T/2 write positions [0, C/2), then the rest), and pass 2
+    // (radix 16, Ns = 16) accumulates its DIF halves v[r], v[r + 8] per round
     dftp<16, true, false>(v);
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-        sts2(buf, 16 * j + r, v[brev<16>(r)]);
-    __syncthreads();
-
-    // inverse pass 2 (radix 16, Ns = 16), outputs r'' in {0, 1, 14, 15} only:
-    // the last pass reads columns j' mod 256 in [0, 32) u [224, 256)
-    {
-        const int k = j & 15;
+    const int k = j & 15;
+    f2 a[8], d[8];
+    if (j < T / 2) {
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            v[r] = lds2(buf, j + T * r);
+            sts2(buf, 16 * j + r, v[brev<16>(r)]);
+    }
+    __syncthreads();
+    f2 h0[8];
 #pragma unroll
-        for (int r = 1; r < 16; r++)
-            v[r] = c_mulconj(v[r], tw256(tt, r, k));
-        f2 a[8], d[8];
+    for (int r = 0; r < 8; r++) {
+        h0[r] = lds2(buf, j + T * r);
+        if (r)
+            h0[r] = c_mulconj(h0[r], tw256(tt, r, k));
+    }
+    __syncthreads();
+    if (j >= T / 2) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            sts2(buf, 16 * j + r - C / 2, v[brev<16>(r)]);
+    }
+    __syncthreads();
+    // pass 2 outputs r'' in {0, 1, 14, 15} only: the last pass reads columns
+    // j' mod 256 in [0, 32) u [224, 256)
+    {
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            a[r] = v[r] + v[r + 8];
-            d[r] = dif_tw<true>(v[r], v[r + 8], 2 * r);
+            const f2 hi = c_mulconj(lds2(buf, j + T * (r + 8) - C / 2), tw256(tt, r + 8, k));
+            a[r] = h0[r] + hi;
+            d[r] = dif_tw<true>(h0[r], hi, 2 * r);
         }
         // X0 = sum a, X1 = sum d, X14 = sum_{r<4} (a_r - a_{r+4}) W_8^r, X15 likewise on d
         f2 x0 = a[0], x1 = d[0], x14 = a[0] - a[4], x15 = d[0] - d[4];
@@ -320,11 +333,13 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
             x15 = x15 + dif_tw<false>(d[r], d[r + 4], 4 * r);
         }
         __syncthreads();
-        const int o = (j >> 4) * 256 + k;
+        // compact: block q = j / 16 of 64 slots holding offsets k, 16 + k,
+        // 224 + k, 240 + k of the 256-column block (lane l of pass 3 reads 64 r + l)
+        const int o = (j >> 4) * 64 + k;
         sts2(buf, o, x0);
         sts2(buf, o + 16, x1);
-        sts2(buf, o + 16 * 14, x14);
-        sts2(buf, o + 16 * 15, x15);
+        sts2(buf, o + 32, x14);
+        sts2(buf, o + 48, x15);
     }
     __syncthreads();
     if (j >= 64)
@@ -336,10 +351,10 @@ __global__ void __launch_bounds__(C / 16, 4) k_pair16(tdoa_kparams kp, tdoa_kout
     const int l = j;
     const int jc = l < 32 ? l : 192 + l;
     const int m = 64 - l;
-    f2 y = lds2(buf, jc);
+    f2 y = lds2(buf, l);
 #pragma unroll
     for (int r = 1; r < R1; r++) {
-        const f2 u = lds2(buf, jc + 256 * r);
+        const f2 u = lds2(buf, 64 * r + l);
         y = y + (l < 32 ? c_mulconj(u, twC(tt, r, jc)) : c_mul(u, twC(tt, r, m)));
     }
     // y[n] = r[2n] + i r[2n+1]: lags 2n, 2n + 1 with n = l or -m
@@ -404,13 +419,14 @@ int launch_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
     if (chunk < 1)
         return tdoa_set_error(-1, "GCC_PHAT: spectrum scratch smaller than one frame");
     const size_t lds = (size_t)(C + C / 16) * sizeof(f2);
+    const size_t lds_pair = (size_t)(C / 2 + C / 32) * sizeof(f2);  // half-size buffer (k_pair16)
     for (int64_t c0 = 0; c0 < B; c0 += chunk) {
         const int64_t nf = (B - c0) < chunk ? (B - c0) : chunk;
         if (nf * P > INT_MAX)
             return tdoa_set_error(-1, "GCC_PHAT: chunk too large for one launch");
         hipLaunchKernelGGL(k_spec16<C>, dim3((unsigned)(nf * M)), dim3(C / 16), lds, st, kp, frames, c0 * M,
                            (f2 *)scratch, e2);
-        hipLaunchKernelGGL(k_pair16<C>, dim3((unsigned)(nf * P)), dim3(C / 16), lds, st, kp, out,
+        hipLaunchKernelGGL(k_pair16<C>, dim3((unsigned)(nf * P)), dim3(C / 16), lds_pair, st, kp, out,
                            (const f2 *)scratch, c0, nf * P);
     }
     if (out.gate) {

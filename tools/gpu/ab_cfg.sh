@@ -1,4 +1,5 @@
-# A/B of bench config 5 and config-2 DIRECT across library variants (tdoa/libtdoa_alt_*.so) vs the default build.
+# A/B of bench configs (CFGS, default "5 2d") across library variants (tdoa/libtdoa_alt_*.so) vs the default build.
+# "2d" = config 2 on the DIRECT engine.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out/ab
 run() {
@@ -8,6 +9,8 @@ run() {
 }
 for f in audio-triangulation_amd/tdoa/libtdoa.so audio-triangulation_amd/tdoa/libtdoa_alt_*.so; do
   n=$(basename $f .so)
-  run $n $f --config 5 || exit 1
-  run $n $f --engine direct --steps 200 || exit 1
+  for c in ${CFGS:-5 2d}; do
+    if [ "$c" = "2d" ]; then run $n $f --engine direct --steps 200 || exit 1
+    else run $n $f --config $c || exit 1; fi
+  done
 done
