@@ -117,6 +117,8 @@ PHAT_CONFIGS = [
     (4, 4096, 50000, synth.square_mics(0.15), 40),
     (8, 2048, 50000, synth.circle_mics(8, 0.15), 40),
     (3, 4096, 48000, None, 40),
+    (2, 4096, 50000, TWO, 40),                             # long-frame kernels, 1 pair
+    (4, 2048, 67600, synth.square_mics(0.15), 40),         # S = 63: lags -63..63, the widest K
     (5, 1024, 50000, synth.circle_mics(5, 0.15), 64),
     (4, 256, 50000, synth.square_mics(0.15), 64),
 ]

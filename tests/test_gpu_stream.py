@@ -118,3 +118,19 @@ def test_stream_reference_trace_fixture(loc48, oracle):
             assert (r["lags"] == g["orc_lags"][s, i]).all()
             if r["gate"]:
                 assert r["cell"] == g["orc_cell"][s, i]
+
+
+@pytest.mark.parametrize("N,hop,M", [(512, 256, 3), (2048, 1024, 3), (1024, 512, 4)])
+def test_stream_register_trigger_shapes(oracle, N, hop, M):
+    """frame_len = 2 x hop runs the register trigger scan (k_stream_trigger_w)
+    for each (G = hop/64, M) it is instantiated for; config 5 is N 1024 / hop 512
+    / 3 mics (test_stream_vs_oracle)."""
+    mics = synth.square_mics(0.15) if M == 4 else None
+    loc = Localizer(sample_rate_hz=48000, frame_len=N, num_mics=M, mic_xy=mics)
+    lut = loc.lut()
+    T = (12 * N // hop) * hop
+    adc = synth.adc_stream(6, T, M, lut, loc.dims.S, 70 + N + M).numpy()
+    recs, est, last = run_pipeline(loc, adc, hop)
+    exp = oracle.stream_run(adc, N, 48000, loc.dims.S, loc.window(), lut)
+    compare(recs, est, last, exp, loc.dims.P)
+    loc.close()
