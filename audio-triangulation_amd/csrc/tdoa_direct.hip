@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include "tdoa_internal.h"
 #include "tdoa_device.h"
@@ -69,6 +70,132 @@ __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
     argmax_prior_phase<int64_t>(kp, sm.scores, sm.best, out, f0, nf);
     DIAG_STAMP(3);
     DIAG_STAMP(4);  // grid solve runs in k_grid (tdoa_grid.hip)
+}
+
+// ------------------------------------------------ exact xcorr on the matrix cores
+// k_direct_mfma: the same stage / argmax / prior / gate as k_direct, with the
+// int64 cross-correlation (correlations.c:9-18) on v_mfma_i32_16x16x64_i8.
+//   Offset byte limbs: every int16 x is stored as z = x ^ 0x0080, whose high
+//   byte h = x >> 8 and low byte l = (x & 255) - 128 are int8 with
+//   x' = x - 128 = 256 h + l.  a'.b' = 65536 ah.bh + 256 (ah.bl + al.bh)
+//   + al.bl; each limb product accumulates exactly in int32 (<= 2 (N+64) 128^2).
+//   Lag s = 16 (n - n0) + w is C[w][n] of a Toeplitz product summed over
+//   NB 64-sample blocks beta:  A[w][k] = a[64 beta + k - w],  B[k][n] =
+//   b[64 beta + k + 16 (n - n0)]  (every i = 64 beta + k - w once), over a
+//   window of L = 64 NB indices that holds the whole a-row and b[16 (n - n0)..N).
+//   Padding (x = 0) is z = 0x0080, so over the window
+//   sum a b = sum a'b' + 128 (sum a + sum_window b) - 128^2 L  exactly.
+// Lane l holds A row w = l & 15, B column n = l & 15, k = 16 (l >> 4) + j in
+// byte j of its 16-byte operands (A and B pair byte for byte), and C rows
+// 4 (l >> 4) + e of column l & 15.
+constexpr int MF_PADW = 96;  // zero words each side of a staged row (b reads reach N + 175 samples)
+
+typedef int v4i_mf __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i_mf mf_limbs(const uint32_t (&w)[8], uint32_t sel)
+{
+    v4i_mf r;
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+        r[d] = (int)__builtin_amdgcn_perm(w[2 * d + 1], w[2 * d], sel);
+    return r;
+}
+
+template <bool PREPARED>
+__global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
+                                                      const int16_t *__restrict__ frames, int64_t B,
+                                                      const int32_t *__restrict__ count, int n0, int nq,
+                                                      int rsum_off)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Smem sm = carve(smem, kp, blockDim.x >> 6);
+    const int64_t f0 = (int64_t)blockIdx.x * kp.F;
+    if (count) {  // batch size known on the device only (streaming pipeline)
+        const int64_t c = *count;
+        B = c < B ? c : B;
+        if (f0 >= B)
+            return;
+    }
+    const int nf = (int)((B - f0) < kp.F ? (B - f0) : kp.F);
+    stage_frames<PREPARED>(kp, sm, frames, f0, nf);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const int RS = kp.RS, rows = nf * kp.M, words = rows * RS;
+    // per row: sum of the row and of its first 16 / 32 / 48 samples (one wave a row)
+    int *rsum = reinterpret_cast<int *>(smem + rsum_off);
+    for (int row = wave; row < rows; row += nwaves) {
+        const uint32_t *x = sm.X + row * RS + kp.PADW;
+        const int v0 = sum_word(x[lane]);
+        int t = v0;
+        for (int i = lane + 64; i < kp.N / 2; i += 64)
+            t += sum_word(x[i]);
+        int p16 = lane < 8 ? v0 : 0, p32 = lane < 16 ? v0 : 0, p48 = lane < 24 ? v0 : 0;
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            t += __shfl_xor(t, m, 64);
+            p16 += __shfl_xor(p16, m, 64);
+            p32 += __shfl_xor(p32, m, 64);
+            p48 += __shfl_xor(p48, m, 64);
+        }
+        if (lane == 0) {
+            rsum[4 * row + 0] = t;
+            rsum[4 * row + 1] = p16;
+            rsum[4 * row + 2] = p32;
+            rsum[4 * row + 3] = p48;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+        sm.X[i] ^= 0x00800080u;
+    __syncthreads();
+
+    const int g = lane >> 4, r = lane & 15, rr = r < nq ? r : nq - 1;
+    const int K = kp.K, S = kp.S, P = kp.P, NB = kp.N / 64 + 1;
+    for (int it = wave; it < nf * P; it += nwaves) {
+        const int f = it / P, p = it - f * P;
+        const int rowa = f * kp.M + kp.pair_i[p], rowb = f * kp.M + kp.pair_j[p];
+        const uint32_t *ra = sm.X + rowa * RS + kp.PADW;  // word of sample 0
+        const uint32_t *rb = sm.X + rowb * RS + kp.PADW;
+        v4i_mf hh = {0, 0, 0, 0}, xx = {0, 0, 0, 0}, ll = {0, 0, 0, 0};
+        for (int beta = 0; beta < NB; beta++) {
+            // A: samples q0 .. q0 + 15, q0 = 64 beta + 16 g - w (w = r; may be odd / negative)
+            const int q0 = 64 * beta + 16 * g - r;
+            const int wa = q0 >> 1;
+            const uint32_t sh = (uint32_t)(q0 & 1) * 2u;
+            uint32_t u[9], aw[8], bw[8];
+#pragma unroll
+            for (int m = 0; m < 9; m++)
+                u[m] = ra[wa + m];
+#pragma unroll
+            for (int m = 0; m < 8; m++)
+                aw[m] = __builtin_amdgcn_alignbyte(u[m + 1], u[m], sh);
+            // B: samples 64 beta + 16 (g + n - n0) .. + 15 (even start)
+            const int wb = 32 * beta + 8 * (g + rr - n0);
+#pragma unroll
+            for (int m = 0; m < 8; m++)
+                bw[m] = rb[wb + m];
+            const v4i_mf ah = mf_limbs(aw, 0x07050301u), al = mf_limbs(aw, 0x06040200u);
+            const v4i_mf bh = mf_limbs(bw, 0x07050301u), bl = mf_limbs(bw, 0x06040200u);
+            hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bh, hh, 0, 0, 0);
+            xx = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bl, xx, 0, 0, 0);
+            xx = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bh, xx, 0, 0, 0);
+            ll = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bl, ll, 0, 0, 0);
+        }
+        if (r < nq) {
+            // 128 (sum a + sum_window b) - 128^2 L; the b window starts at 16 (r - n0)
+            const int d = r - n0;
+            const int sb = rsum[4 * rowb] - (d > 0 ? rsum[4 * rowb + d] : 0);
+            const int64_t corr = 128 * ((int64_t)rsum[4 * rowa] + sb) - (int64_t)16384 * 64 * NB;
+            int64_t *dst = sm.scores + (size_t)(f * P + p) * K + S;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int sl = 16 * (r - n0) + 4 * g + e;
+                if (sl >= -S && sl <= S)
+                    dst[sl] = (int64_t)hh[e] * 65536 + (int64_t)xx[e] * 256 + (int64_t)ll[e] + corr;
+            }
+        }
+    }
+    __syncthreads();
+    argmax_prior_phase<int64_t>(kp, sm.scores, sm.best, out, f0, nf);
 }
 
 // --------------------------------------------------------------- EMA
@@ -262,6 +389,36 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
     tdoa_kparams kp = kp_in;
     int threads = 0;
+    // matrix-core path (k_direct_mfma): TDOA_DIRECT_MFMA=0 keeps the VALU kernel (A/B)
+    static const int use_mfma = [] {
+        const char *s = getenv("TDOA_DIRECT_MFMA");
+        return s ? atoi(s) : 1;
+    }();
+    if (use_mfma && kp.N % 64 == 0 && kp.N >= 64 && kp.S <= 63) {
+        const int n0 = (kp.S + 15) / 16, nq = n0 + (kp.S + 1 + 15) / 16;  // lag columns -16 n0 .. 16 (nq - n0) - 1
+        kp.PADW = MF_PADW;
+        kp.RS = kp.N / 2 + 2 * MF_PADW;
+        kp.F = kp.P >= 16 ? 1 : 16 / kp.P > 4 ? 4 : 16 / kp.P;  // frames per workgroup: one wave per (frame, pair) up to 16
+        threads = 64 * (kp.F * kp.P < 16 ? kp.F * kp.P : 16);
+        const size_t rsum_off = smem_bytes(kp, threads / 64);
+        const size_t lds = rsum_off + (size_t)16 * kp.F * kp.M;
+        if (lds > 160 * 1024)
+            return tdoa_set_error(-1, "DIRECT: shape needs more than 160 KiB LDS per workgroup");
+        if (lds_bytes_out)
+            *lds_bytes_out = (int)lds;
+        const int64_t grid = (B + kp.F - 1) / kp.F;
+        if (grid > INT_MAX)
+            return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
+        hipStream_t st = (hipStream_t)stream;
+        if (prepared)
+            hipLaunchKernelGGL((k_direct_mfma<true>), dim3((unsigned)grid), dim3(threads), lds, st, kp, out, frames,
+                               B, count_dev, n0, nq, (int)rsum_off);
+        else
+            hipLaunchKernelGGL((k_direct_mfma<false>), dim3((unsigned)grid), dim3(threads), lds, st, kp, out, frames,
+                               B, count_dev, n0, nq, (int)rsum_off);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "k_direct_mfma launch");
+    }
     direct_geometry(kp, threads);
     const size_t lds = smem_bytes(kp, threads / 64);
     if (lds > 160 * 1024)
