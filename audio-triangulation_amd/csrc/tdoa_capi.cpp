@@ -21,6 +21,8 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -420,7 +422,20 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             }
             c->win[i] = cfg->window_q15[i];
         }
+    } else if (N < 1024 && 1024 % N == 0) {
+        // buffer.c:8 indexes WINDOW_FUNCTION[i << (10 - BUFFER_SIZE_BITS)]: a
+        // shorter frame subsamples the 1024-point Q15 table
+        std::vector<int32_t> w1k(1024);
+        int rc = tdoa_dpss_q15(1024, 2.0, w1k.data());
+        if (rc) {
+            delete c;
+            return rc;
+        }
+        for (int i = 0; i < N; i++)
+            c->win[i] = w1k[(size_t)i * (1024 / N)];
     } else {
+        // N > 1024 (where buffer.c:8 is undefined): DPSS(N, NW=2) by the
+        // window.ipynb procedure
         int rc = tdoa_dpss_q15(N, 2.0, c->win.data());
         if (rc) {
             delete c;
@@ -636,6 +651,25 @@ static int grow(void **p, size_t *have, size_t need, void *stream, const char *w
         return fail(TDOA_ERR_NOMEM, "%s scratch of %zu bytes", what, need);
     *have = need;
     return TDOA_OK;
+}
+
+int tdoa_resident_blocks(const void *kernel, int threads, size_t lds)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void *, int, size_t>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(dev, kernel, threads, lds);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end())
+        return it->second;
+    int per_cu = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds);
+    const int r = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+    cache[key] = r;
+    return r;
 }
 
 static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,

@@ -709,21 +709,7 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         // + grid tail: [3][128][8] scores, 8 frame indices, [3][8] reductions
         const size_t lds1024 = 7 * 1024 * 8 + 514 * 8 + 512 * 8 + 8 * 4 + 3 * 128 * GSLOTS * 4 +
                                GSLOTS * 8 + 3 * GSLOTS * 8;
-        // resident workgroups for this LDS size (cached per device / size)
-        static int c_dev = -1, c_resident = 0;
-        static size_t c_lds = 0;
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (dev != c_dev || lds1024 != c_lds) {
-            int per_cu = 0, cus = 0;
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gcc_phat_1024, 192,
-                                                              lds1024);
-            c_resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
-            c_dev = dev;
-            c_lds = lds1024;
-        }
-        const int resident = c_resident;
+        const int resident = tdoa_resident_blocks((const void *)k_gcc_phat_1024, 192, lds1024);
         const int64_t npairs = (B + 1) / 2;
         const int64_t iters = (npairs + resident - 1) / resident;
         const int64_t grid = (npairs + iters - 1) / iters;

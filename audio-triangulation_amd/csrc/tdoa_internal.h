@@ -96,6 +96,11 @@ struct tdoa_stream_kout {
     int64_t *max_L;
 };
 
+// Resident workgroups of `kernel` (threads, dynamic LDS) on the current device:
+// blocks per CU from the occupancy query x CUs, cached per (device, kernel,
+// threads, LDS) under a mutex (contexts on different host threads / devices).
+int tdoa_resident_blocks(const void *kernel, int threads, size_t lds);
+
 // Host-side launchers implemented in the .hip files.
 // count_dev (optional): device int32 batch size, B then only bounds the grid.
 int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,

@@ -108,6 +108,10 @@ __device__ __forceinline__ void sts_f2(char *base, int off, f2 v)
     *reinterpret_cast<f2 *>(base + off) = v;
 }
 
+// an empty asm that needs the value: it must be computed here (keeps IR
+// passes from sinking a finished partial sum past later phases)
+__device__ __forceinline__ void pin(f2 &x) { asm volatile("" : "+v"(x)); }
+
 __device__ __forceinline__ f2 unit(f2 x, float e2)
 {
     return x * __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
@@ -674,6 +678,381 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// k_p1k_lean: the same per-frame algorithm at TWO waves per SIMD (8 waves per
+// workgroup, one workgroup per CU, <= 256 registers per lane).  One frame per
+// half-wave and one FFT stream; the register plan keeps at most two unit
+// spectra plus one working column live:
+//   mic 0 -> U0, mic 1 -> U1, pair (0,1) built straight into the inverse's
+//   column (no third spectrum), mic 2 -> V, U0 <- conj(U0) V, U1 <- conj(U1) V,
+//   pairs (0,2), (1,2).
+// Table values (window, twiddles) are read from LDS next to their use instead
+// of as whole per-phase arrays.  The grid solve runs per iteration on the
+// wave's two frames (b64 gathers of an [p][k] f2 score table).  The partner
+// wave of the SIMD hides the LDS round trips that bound the one-wave kernel.
+namespace {
+
+// front end + forward FFT_1024 of one mic row, then the partner swap: V[k],
+// V[31 - k] hold Z[b], Z[N - b] (paired layout); V[32] = unit X[512] (lane 0)
+__device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)[16], f2 (&V)[33],
+                                              float e2)
+{
+    f2 v[32];
+    {
+        int s = 0;
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            s = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_t, w[t]), v2s_t{1, 1}, s, false);
+        s = hsum32(s, L.hw);
+        const uint32_t off = (uint32_t)(s >> 10) & 0xFFu;
+        const uint32_t off2 = off | (off << 16);
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const f2 wf = lds_f2(L.win, 8 * L.cs + 256 * t);
+            const uint32_t d = (w[t] | 0x01000100u) - off2;
+            const float s0 = (float)(int8_t)(d & 0xFFu);
+            const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+            v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
+        }
+    }
+    fft_col_lds<false, true>(L, v, L.tileA);
+    fft_row_fwd(L, L.tileA, V);
+    V[32] = c_unit(conjf2(V[16]), e2);
+#pragma unroll
+    for (int j = 16; j < 32; j++) {
+        const f2 t = dpp_xor1(V[j]);
+        const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
+        V[j] = (L.is0 || L.is1) ? own : t;
+    }
+}
+
+// real-FFT split of the partner pair k + unit normalisation: the unit
+// spectrum at bins b and N - b (the W_2048^b twiddle read next to its use)
+__device__ __forceinline__ void lean_split(const Lane &L, f2 A, f2 Bv, int k, float e2, f2 &ub,
+                                           f2 &un)
+{
+    const f2 wk = lds_f2(L.tw2, 8 * L.cs + 256 * k);
+    const f2 e = c_addconj(A, Bv);
+    const f2 od = c_mul(c_subconj(A, Bv), wk);
+    ub = c_unit(c_add_mi(e, od), e2);
+    un = c_unit(c_conj_add_i(e, od), e2);
+}
+
+// unit spectrum of one mic row, in place (paired layout)
+__device__ __forceinline__ void lean_forward(const Lane &L, const uint32_t (&w)[16], f2 (&U)[33],
+                                             float e2)
+{
+    lean_spectrum(L, w, U, e2);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        lean_split(L, U[k], U[31 - k], k, e2, U[k], U[31 - k]);
+}
+
+// unit spectrum V of one mic row consumed bin pair by bin pair as it is
+// produced: A <- conj(A) V, B <- conj(B) V (V is never whole after the split)
+__device__ __forceinline__ void lean_forward_cross(const Lane &L, const uint32_t (&w)[16],
+                                                   f2 (&A)[33], f2 (&Bs)[33], float e2)
+{
+    f2 V[33];
+    lean_spectrum(L, w, V, e2);
+    A[32] = c_conjmul(A[32], V[32]);
+    Bs[32] = c_conjmul(Bs[32], V[32]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        f2 ub, un;
+        lean_split(L, V[k], V[31 - k], k, e2, ub, un);
+        A[k] = c_conjmul(A[k], ub);
+        A[31 - k] = c_conjmul(A[31 - k], un);
+        Bs[k] = c_conjmul(Bs[k], ub);
+        Bs[31 - k] = c_conjmul(Bs[31 - k], un);
+    }
+}
+
+// second half of the pruned inverse (fft_row_inv) in two groups of 8 residue
+// pairs, so at most half a row of tile values is in registers at a time
+__device__ __forceinline__ void lean_row_inv(const Lane &L, const char *tile, f2 &y0, f2 &y31)
+{
+    const int ro = P1K_ROW * L.cs;
+    f2 ga[2], gd[2];
+#pragma unroll
+    for (int g = 0; g < 2; g++) {
+        f2 a[8], d[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const f2 v = lds_f2(tile, ro + 8 * slot(8 * g + i));
+            const f2 u = lds_f2(tile, ro + 8 * slot(8 * g + i + 16));
+            a[i] = v + u;
+            d[i] = tw_only<false>(v - u, 8 * g + i);
+        }
+#pragma unroll
+        for (int h = 4; h >= 1; h >>= 1)
+#pragma unroll
+            for (int r = 0; r < h; r++) {
+                a[r] = a[r] + a[r + h];
+                d[r] = d[r] + d[r + h];
+            }
+        ga[g] = a[0];
+        gd[g] = d[0];
+        pin(ga[g]);
+        pin(gd[g]);
+    }
+    y0 = ga[0] + ga[1];
+    y31 = gd[0] + gd[1];
+}
+
+// residue of lane l (lane_res) in plain arithmetic (no divergent branch)
+__device__ __forceinline__ int lane_res_sel(int l)
+{
+    const int h = l >> 1, o = l & 1;
+    return h + o * (32 - 2 * h) - ((l == 1) << 4);
+}
+
+
+// the lane id through an opaque move: lane-dependent values derived from it
+// are computed where they are used instead of being hoisted to the kernel's
+// start and held in registers across every phase
+__device__ __forceinline__ int fresh_tid()
+{
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+// packed inverse input of the cross spectrum R (paired layout; R[k] =
+// conj(A[k]) B[k] when B is given, else R = A), back in residue columns
+template <bool CROSS>
+__device__ __forceinline__ void lean_pretwiddle(const Lane &L, const f2 (&A)[33], const f2 (&Bs)[33],
+                                                f2 (&v)[32])
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const f2 Rk = CROSS ? c_conjmul(A[k], Bs[k]) : A[k];
+        const f2 Rn = CROSS ? c_conjmul(A[31 - k], Bs[31 - k]) : A[31 - k];
+        const f2 wk = lds_f2(L.tw2, 8 * L.cs + 256 * k);
+        const f2 s = c_addconj(Rk, Rn);
+        const f2 q = c_mulconj(c_subconj(Rk, Rn), wk);
+        v[k] = c_add_i(s, q);
+        v[31 - k] = c_conj_add_mi(s, q);
+    }
+    const f2 R32 = CROSS ? c_conjmul(A[32], Bs[32]) : A[32];
+    const f2 Ye = f2{2.0f * R32.x, -2.0f * R32.y};  // Y[512] = 2 conj(R[512])
+#pragma unroll
+    for (int j = 31; j >= 16; j--) {
+        const f2 t = dpp_xor1(v[j]);
+        const f2 own = L.is0 ? (j == 16 ? Ye : v[j - 1]) : v[j];
+        v[j] = (L.is0 || L.is1) ? own : t;
+    }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout out,
+                                                     const int16_t *__restrict__ frames, int64_t B,
+                                                     float e2)
+{
+    constexpr int N = 1024, P = 3, NW = 8, NF = 2 * NW, NT = NW * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *tiles = smem;                               // [NW][2][TILE]
+    char *twm = tiles + NW * 2 * P1K_TILE;            // [32][32] f2
+    char *tw2 = twm + 32 * 32 * 8;                    // [16][32] f2
+    char *win = tw2 + 16 * 32 * 8;                    // [512] f2
+    const float *prior = (const float *)(win + 512 * 8);  // [128]
+    const uint32_t *tups = (const uint32_t *)(prior + 128);
+
+    const int tid = threadIdx.x, wave = tid >> 6, hw = (tid >> 5) & 1, lane64 = tid & 63;
+    Lane L;
+    L.hw = hw;
+    L.lane = tid & 31;
+    L.res = lane_res(L.lane);
+    L.cs = slot(L.res);
+    L.is0 = L.lane == 0;
+    L.is1 = L.lane == 1;
+    char *wtiles = tiles + wave * 2 * P1K_TILE;
+    L.tileA = wtiles + hw * P1K_TILE;
+    L.tileB = L.tileA;
+    L.twm = twm;
+    L.tw2 = tw2;
+    L.win = win;
+
+    const int K = kp.K, S = kp.S;
+    const bool do_grid = out.cell || out.xy || out.max_Lf;
+    const int Upad = (kp.U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
+
+    auto fetch = [&](uint32_t(&w)[16], int64_t fr, int m) {
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(
+            frames + ((fr < B ? fr : B - 1) * 3 + m) * (int64_t)N) + L.res;
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            w[t] = __builtin_nontemporal_load(row + 32 * t);
+    };
+    {
+        const uint4 *src = (const uint4 *)kp.p1k_img;
+        uint4 *dst = (uint4 *)twm;
+        const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
+#pragma unroll 4
+        for (int e = tid; e < n16; e += NT)
+            dst[e] = src[e];
+    }
+    __syncthreads();
+
+    const float invL = 1.0f / 2048.0f;
+
+    const int64_t stride = (int64_t)gridDim.x * NF;
+    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += stride) {
+        const int64_t f = base + 2 * wave + hw;
+        const bool live = f < B;
+        uint32_t w0[16], w1[16], w2[16];
+        fetch(w0, f, 0);
+        fetch(w1, f, 1);
+        float wv[3][4];
+        int best[3];
+        auto finish_pair = [&](int p, f2 y0, f2 y31) {
+            // this lane's four candidate lags (recomputed here, see fresh_tid)
+            const int ft = fresh_tid();
+            const int fres = lane_res_sel(ft & 31), fhw = (ft >> 5) & 1;
+            const int la = 2 * fres, lb = 2 * fres - 64;
+            const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
+            const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
+            const float cv[4] = {y31.x * invL, y31.y * invL, y0.x * invL, y0.y * invL};
+            float bv = -INFINITY;
+            int bk = INT_MAX;
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (ok[c] && (cv[c] > bv || bk == INT_MAX)) {
+                    bv = cv[c];
+                    bk = ck[c];
+                }
+            half_argmax_to31(bv, bk);
+            const int b0 = __builtin_amdgcn_readlane(bk, 31), b1 = __builtin_amdgcn_readlane(bk, 63);
+            bk = fhw ? b1 : b0;
+            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
+            best[p] = bk - S;
+            const int64_t ff = base + 2 * ((ft >> 6) & 7) + fhw;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int d = ck[c] > bk ? ck[c] - bk : bk - ck[c];
+                wv[p][c] = ok[c] ? cv[c] * prior[ok[c] ? d : 0] : 0.0f;
+                if (ff < B && ok[c]) {
+                    const size_t gb = (size_t)(ff * P + p) * K;
+                    if (out.scores_f)
+                        out.scores_f[gb + ck[c]] = cv[c];
+                    if (out.weighted_f)
+                        out.weighted_f[gb + ck[c]] = wv[p][c];
+                }
+            }
+            if (ff < B && (ft & 31) == 0)
+                out.lags[ff * P + p] = bk - S;
+        };
+
+        f2 U0[33], U1[33], y0, y31;
+        lean_forward(L, w0, U0, e2);
+        lean_forward(L, w1, U1, e2);
+        {
+            f2 v[32];
+            lean_pretwiddle<true>(L, U0, U1, v);  // pair 0: (0, 1)
+            fft_col_lds<true, false>(L, v, L.tileA);
+            // mic 2's words: fetched after the pair's column pass, the kernel's
+            // register peak (two unit spectra + a working column)
+            fetch(w2, f, 2);
+            lean_row_inv(L, L.tileA, y0, y31);
+        }
+        finish_pair(0, y0, y31);
+        lean_forward_cross(L, w2, U0, U1, e2);  // pairs 1: (0, 2), 2: (1, 2)
+        {
+            f2 v[32];
+            lean_pretwiddle<false>(L, U0, U0, v);
+            fft_col_lds<true, false>(L, v, L.tileA);
+            lean_row_inv(L, L.tileA, y0, y31);
+        }
+        finish_pair(1, y0, y31);
+        {
+            f2 v[32];
+            lean_pretwiddle<false>(L, U1, U1, v);
+            fft_col_lds<true, false>(L, v, L.tileA);
+            lean_row_inv(L, L.tileA, y0, y31);
+        }
+        finish_pair(2, y0, y31);
+        if (live && L.lane == 0 && out.gate)
+            out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
+
+        if (!do_grid)
+            continue;
+        // ---- grid solve (vga_heatmap.h:99-108) of the wave's two frames:
+        // weighted scores [p][KPAD] f2 (frame hw in component hw) in the wave's
+        // tile space, lanes split the distinct lag tuples (4 consecutive per
+        // lane and step, ascending: a strict '>' keeps the first maximum)
+        float *wsc = (float *)wtiles;  // [P][KPAD][2]
+        const int gres = lane_res_sel(fresh_tid() & 31);
+        const int gla = 2 * gres, glb = 2 * gres - 64;
+        const int ck[4] = {glb + S, glb + 1 + S, gla + S, gla + 1 + S};
+        const bool ok[4] = {glb >= -S, glb + 1 >= -S, gla <= S, gla + 1 <= S};
+#pragma unroll
+        for (int p = 0; p < P; p++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (ok[c])
+                    wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
+        if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
+            wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
+        float gv[2] = {-INFINITY, -INFINITY};
+        int gu[2] = {INT_MAX, INT_MAX};
+        const char *ws = (const char *)wsc;
+        const uint4 *tq = (const uint4 *)tups;
+        uint4 q = tq[lane64];
+        for (int u0 = 0; u0 < Upad; u0 += 256) {
+            const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
+            f2 Lg[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                // tuple fields are byte offsets of f2 slots in [p][KPAD]
+                const f2 l0 = lds_f2(ws, (int)(wq[i] & 0x3FFu));
+                const f2 l1 = lds_f2(ws, P1K_KPAD * 8 + (int)((wq[i] >> 10) & 0x3FFu));
+                const f2 l2 = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(wq[i] >> 20));
+                Lg[i] = (l0 + l1) + l2;
+            }
+            q = tq[(u0 + 256 < Upad ? u0 + 256 : u0) / 4 + lane64];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int u = u0 + 4 * lane64 + i;
+                if (Lg[i].x > gv[0]) {
+                    gv[0] = Lg[i].x;
+                    gu[0] = u;
+                }
+                if (Lg[i].y > gv[1]) {
+                    gv[1] = Lg[i].y;
+                    gu[1] = u;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+            wave_argmax_to63(gv[j], gu[j]);
+        if (lane64 == 63) {
+            int cells[2];
+#pragma unroll
+            for (int j = 0; j < 2; j++)  // every L compared false (NaN scores): tuple 0
+                cells[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int64_t fs = base + 2 * wave + j;
+                if (fs < B) {
+                    if (out.cell)
+                        out.cell[fs] = cells[j];
+                    if (out.max_Lf)
+                        out.max_Lf[fs] = gv[j];
+                    if (out.xy) {
+                        const int cx = cells[j] % kp.grid_W, cy = cells[j] / kp.grid_W;
+                        out.xy[2 * fs] = (float)(cx - kp.half_w) / kp.grid_scale;
+                        out.xy[2 * fs + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+                    }
+                }
+            }
+        }
+        // the tile space is rewritten by the next iteration's transposes:
+        // every lane's gathers must have landed (same wave: LDS ops in order)
+    }
+}
+
 #ifdef TDOA_DIAG
 extern "C" int tdoa_diag_fetch_p1k(unsigned long long *host, int n)
 {
@@ -702,24 +1081,17 @@ int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
                float e2, hipStream_t st)
 {
     const size_t lds = p1k_lds<NW, DUAL>(kp.U);
-    static int c_dev = -1, c_resident = 0;
-    static size_t c_lds = 0;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev != c_dev || lds != c_lds) {
-        int per_cu = 0, cus = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phat1024<NW, DUAL>, NW * 64, lds);
-        c_resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
-        c_dev = dev;
-        c_lds = lds;
-    }
+    const void *kern = DUAL ? (const void *)k_phat1024<NW, DUAL> : (const void *)k_p1k_lean;
+    const int c_resident = tdoa_resident_blocks(kern, NW * 64, lds);
     constexpr int NF = 2 * NW;
     const int64_t groups = (B + NF - 1) / NF;
     const int64_t iters = (groups + c_resident - 1) / c_resident;
     const int64_t grid = (groups + iters - 1) / iters;
-    hipLaunchKernelGGL((k_phat1024<NW, DUAL>), dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames,
-                       B, e2);
+    if constexpr (DUAL)
+        hipLaunchKernelGGL((k_phat1024<NW, DUAL>), dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out,
+                           frames, B, e2);
+    else
+        hipLaunchKernelGGL(k_p1k_lean, dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames, B, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char buf[256];
@@ -777,7 +1149,7 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp)
 {
     if (g_p1k_waves < 0) {
         const char *s = getenv("TDOA_PHAT1024_WAVES");
-        g_p1k_waves = s ? atoi(s) : 4;
+        g_p1k_waves = s ? atoi(s) : 8;
         if (g_p1k_waves != 0 && g_p1k_waves != 4 && g_p1k_waves != 8)
             g_p1k_waves = 8;
     }

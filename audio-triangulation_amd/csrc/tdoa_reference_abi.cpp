@@ -17,7 +17,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -33,8 +35,8 @@ point2d_t mic_c_location;
 
 static_assert(sizeof(struct buffer_t) == 2056, "buffer_t layout (x86-64)");
 static_assert(sizeof(struct correlations_t) == 760, "correlations_t layout (x86-64)");
-static_assert(sizeof(struct rolling_buffer_t) == 2088 || sizeof(struct rolling_buffer_t) == 2096,
-              "rolling_buffer_t layout");
+static_assert(sizeof(struct rolling_buffer_t) == 2096, "rolling_buffer_t layout (x86-64)");
+static_assert(offsetof(struct rolling_buffer_t, buffer) == 42, "rolling_buffer_t.buffer offset");
 
 namespace {
 
@@ -52,7 +54,7 @@ int g_device = 0;
 // staging buffers; the reference's functions are single-threaded, guard anyway.
 struct RefState {
     std::mutex mu;
-    bool ready = false;
+    std::atomic<bool> ready{false};  // published after the state below (double-checked init)
     tdoa_ctx *ctx = nullptr;
     int16_t *d_frames = nullptr;   // [2][1024]
     int16_t *d_ring = nullptr;     // [1024]
@@ -78,10 +80,10 @@ void check(hipError_t e, const char *what)
 
 RefState &ref()
 {
-    if (g_ref.ready)
+    if (g_ref.ready.load(std::memory_order_acquire))
         return g_ref;
     std::lock_guard<std::mutex> lk(g_ref.mu);
-    if (g_ref.ready)
+    if (g_ref.ready.load(std::memory_order_relaxed))
         return g_ref;
     tdoa_config cfg;
     tdoa_config_default(&cfg);
@@ -104,7 +106,7 @@ RefState &ref()
     for (int i = 0; i < 1024; i++)
         w16[i] = (int16_t)w[i];
     check(hipMemcpy(g_ref.d_window, w16, sizeof w16, hipMemcpyHostToDevice), "hipMemcpy");
-    g_ref.ready = true;
+    g_ref.ready.store(true, std::memory_order_release);
     return g_ref;
 }
 
@@ -138,7 +140,7 @@ extern "C" void tdoa_ref_set_clock(absolute_time_t (*now_us)(void))
 
 extern "C" int tdoa_ref_set_device(int device)
 {
-    if (g_ref.ready)
+    if (g_ref.ready.load(std::memory_order_acquire))
         return TDOA_ERR_INVALID;
     g_device = device;
     return TDOA_OK;

@@ -231,11 +231,15 @@ __global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp,
         if (j >= cl)
             j -= cl;
         // contiguous, and the aligned word reads (up to 7 bytes past the chunk)
-        // stay inside this stream's ring
+        // stay inside this stream's ring.  Word pointer and byte shift both come
+        // from the ABSOLUTE address: a stream's ring starts at s * cl * M, which
+        // need not be 4-byte aligned (M = 3 with an odd capture length); the
+        // aligned start may then lie up to 3 bytes before the ring (inside the
+        // previous stream's, the allocation's base being 4-byte aligned)
         if (l0 >= 0 && (j + G) * M + 7 <= cl * M) {
-            const size_t cb = (size_t)j * M;
-            const uint32_t *wp = reinterpret_cast<const uint32_t *>(cap + (cb & ~(size_t)3));
-            const uint32_t sh = (uint32_t)(((uintptr_t)cap + cb) & 3u);
+            const uintptr_t p = (uintptr_t)(cap + (size_t)j * M);
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(p & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(p & 3u);
             uint32_t w[CW + 1];
 #pragma unroll
             for (int k = 0; k <= CW; k++)

@@ -120,14 +120,17 @@ class Localizer:
 
     # ---------------------------------------------------------- compute
     def alloc_outputs(self, B: int, scores: bool = False, grid: bool = True,
-                      ls: bool = False) -> dict:
+                      ls: bool = False, engine: str | None = None) -> dict:
+        """Output tensors for a batch of B frames; `engine` overrides the
+        context's (the prepared path always fills the DIRECT int64 set)."""
         dev, P, K = self.torch_device, self.dims.P, self.dims.K
+        direct = (engine or self.engine) == "direct"
         o = {"lags": torch.empty((B, P), dtype=torch.int32, device=dev),
              "gate": torch.empty(B, dtype=torch.uint8, device=dev)}
         if grid:
             o["cell"] = torch.empty(B, dtype=torch.int32, device=dev)
             o["xy"] = torch.empty((B, 2), dtype=torch.float32, device=dev)
-            if self.engine == "direct":
+            if direct:
                 o["max_L"] = torch.empty(B, dtype=torch.int64, device=dev)
             else:
                 o["max_Lf"] = torch.empty(B, dtype=torch.float32, device=dev)
@@ -135,7 +138,7 @@ class Localizer:
             o["xy_ls"] = torch.empty((B, 2), dtype=torch.float32, device=dev)
             o["ls_rms"] = torch.empty(B, dtype=torch.float32, device=dev)
         if scores:
-            if self.engine == "direct":
+            if direct:
                 o["scores"] = torch.empty((B, P, K), dtype=torch.int64, device=dev)
                 o["weighted"] = torch.empty((B, P, K), dtype=torch.int64, device=dev)
             else:
@@ -178,9 +181,11 @@ class Localizer:
 
     def correlate_prepared(self, prepared: torch.Tensor, scores: bool = True,
                            grid: bool = True) -> dict:
-        """Frames already DC-removed, normalised and windowed (correlations_init inputs)."""
+        """Frames already DC-removed, normalised and windowed (correlations_init
+        inputs).  Runs the reference's integer path (DIRECT) on any context, so
+        the int64 outputs are returned whatever the context's engine."""
         B = self._check_frames(prepared)
-        out = self.alloc_outputs(B, scores=scores, grid=grid)
+        out = self.alloc_outputs(B, scores=scores, grid=grid, engine="direct")
         s = self._outputs_struct(out)
         st = torch.cuda.current_stream(self.torch_device)
         check(load().tdoa_correlate_prepared(self._ctx, C.c_void_p(prepared.data_ptr()), B,

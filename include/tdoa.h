@@ -74,9 +74,11 @@ typedef struct tdoa_config {
     int32_t grid_half_h;     /* 50 */
     float grid_scale;        /* 24.0f */
     float height_offset;     /* 1.2f */
-    /* Q15 window [N]; NULL -> DPSS(N, NW=2) normalised to max 1, x32767,
-     * rounded (window.ipynb procedure; equals window_function.h at N=1024).
-     * Copied. */
+    /* Q15 window [N]; NULL -> the reference's table: for N <= 1024 the
+     * 1024-point DPSS(NW=2) table (window_function.h) subsampled as
+     * buffer.c:8 indexes it, W[i << (10 - log2 N)]; for N > 1024 (where
+     * buffer.c:8 is undefined) DPSS(N, NW=2) normalised to max 1, x32767,
+     * rounded (window.ipynb procedure).  Copied. */
     const int32_t *window_q15;
     float phat_eps;          /* GCC_PHAT: floor of |X_i^* X_j| (samples scaled by 2^-15), default 1e-12 */
 } tdoa_config;

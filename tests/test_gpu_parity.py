@@ -229,3 +229,32 @@ def test_plain_c_host_program():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "lags ab=5 ac=9 bc=4" in r.stdout
     assert "recovered all three injected lags" in r.stdout
+
+
+@pytest.mark.parametrize("N", [256, 512, 1024])
+def test_default_window_is_reference_table(N):
+    """N <= 1024: the 1024-point table subsampled as buffer.c:8 indexes it,
+    WINDOW_FUNCTION[i << (10 - BUFFER_SIZE_BITS)] (pinned to window_function.h
+    in test_oracle_pin.py)."""
+    loc = Localizer(frame_len=N)
+    w1k = golden("window_q15.npz")["n1024"]
+    assert (loc.window() == w1k[::1024 // N]).all()
+    loc.close()
+
+
+def test_correlate_prepared_on_gcc_phat_context_returns_direct_outputs(oracle):
+    """correlations_init inputs run the reference's integer path whatever the
+    context's engine: the call returns the int64 outputs it filled."""
+    loc = Localizer(engine="gcc_phat")
+    g = torch.Generator(device="cpu").manual_seed(11)
+    fr = torch.randint(-32768, 32768, (8, 3, 1024), generator=g, dtype=torch.int32)
+    fr = fr.to(torch.int16).cuda()
+    got = _np(loc.correlate_prepared(fr))
+    assert "scores" in got and "weighted" in got and "max_L" in got
+    frn = fr.cpu().numpy()
+    for b in range(frn.shape[0]):
+        for p, (i, j) in enumerate([(0, 1), (0, 2), (1, 2)]):
+            sc, best = oracle.xcorr(frn[b, i], frn[b, j], 46)
+            assert (got["scores"][b, p] == sc).all()
+            assert got["lags"][b, p] == best
+    loc.close()

@@ -22,16 +22,18 @@ def run_pipeline(loc, adc, hop, use_graph=True, capture_len=None):
     if capture_len is None:
         cap = torch.from_numpy(adc).cuda()
     else:  # producer-fed capture ring
-        cap = torch.zeros((S, capture_len, M), dtype=torch.uint8, device="cuda")
+        # + 4 spare bytes: an unaligned last ring may be read word-wise
+        flat = torch.zeros(S * capture_len * M + 4, dtype=torch.uint8, device="cuda")
+        cap = flat[:S * capture_len * M].view(S, capture_len, M)
         src = torch.from_numpy(adc).cuda()
     pipe = StreamPipeline(loc, cap, hop=hop, use_graph=use_graph)
     recs = {s: [] for s in range(S)}
     for h in range(steps):
         if capture_len is not None:
             with torch.cuda.stream(pipe.stream):
-                for t0 in range(h * hop, (h + 1) * hop, hop):
-                    j = t0 % capture_len
-                    cap[:, j:j + hop] = src[:, t0:t0 + hop]
+                t0 = h * hop
+                idx = torch.arange(t0, t0 + hop, device="cuda") % capture_len
+                cap[:, idx] = src[:, t0:t0 + hop]
         pipe.step()
         r = pipe.records()
         for i, s in enumerate(r["stream_id"]):
@@ -87,10 +89,14 @@ def test_stream_graph_equals_eager(loc48):
             assert all((x[k] == y[k]).all() for k in x)
 
 
-def test_stream_capture_ring_wraps(loc48, oracle):
+@pytest.mark.parametrize("capture_len", [2048, 2049, 2051])
+def test_stream_capture_ring_wraps(loc48, oracle, capture_len):
+    """A producer-fed ring; odd lengths make every stream's ring start
+    unaligned (stride capture_len * 3 bytes), which the register trigger scan
+    reads word-wise (byte shift from the absolute address)."""
     lut = loc48.lut()
     adc = synth.adc_stream(6, 512 * 24, 3, lut, loc48.dims.S, 23).numpy()
-    recs, est, last = run_pipeline(loc48, adc, 512, capture_len=2048)
+    recs, est, last = run_pipeline(loc48, adc, 512, capture_len=capture_len)
     exp = oracle.stream_run(adc, 1024, 48000, loc48.dims.S, loc48.window(), lut)
     compare(recs, est, last, exp, loc48.dims.P)
 

@@ -1,0 +1,98 @@
+#!/bin/bash
+# One GPU-box driver for every measurement this repo takes (run through
+# gpurun from the repo root).  Steps run in order and the script stops at the
+# first failure; every GPU step has its own time limit.
+#
+#   tools/gpu/run.sh STEP [STEP ...]
+#
+#   test[:FILES]          pytest -m gpu (FILES comma-separated, default tests/)
+#   ab[:V1,V2,..]         bench config 2 once per TDOA_PHAT1024_WAVES value
+#                         (8 = two-waves-per-SIMD kernel, 4 = one-wave kernel)
+#   bench[:CFG[:ENGINE]]  bench.py line -> gpurun_out/bench_cCFG_ENGINE.json
+#   kstats[:CFG[:ENGINE]] rocprofv3 --kernel-trace --stats of the bench
+#   pmc[:CFG[:ENGINE]]    FETCH_SIZE and WRITE_SIZE passes (one run each)
+#   sq[:CFG[:ENGINE]]     two SQ counter passes (waves, VALU, LDS, waits)
+#   smoke                 __graft_entry__.smoke()
+#
+# Env: TAG (output subdirectory, default "cur"), STEPS (bench steps),
+# BENCH_ARGS (extra bench.py arguments).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 2
+export TMPDIR=/tmp
+TAG=${TAG:-cur}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+ROOT=$GRAFT_REPO_ROOT
+
+field() {  # field N of a colon-separated step, with a default
+    local v
+    v=$(echo "$1" | cut -d: -f"$2")
+    [ "$v" = "$1" ] && [ "$2" != 1 ] && v=""
+    echo "${v:-$3}"
+}
+
+prof() {  # prof NAME ROCPROF-ARGS... -- (bench args follow)
+    local name=$1; shift
+    (cd /tmp && timeout -s KILL 240 rocprofv3 "$@" -d "$ROOT/$OUT/$name" -o run --output-format csv \
+        -- python3 "$ROOT/bench.py" $PARGS > "$ROOT/$OUT/$name.log" 2>&1)
+}
+
+for step in "$@"; do
+    kind=$(field "$step" 1)
+    case $kind in
+    test)
+        files=$(field "$step" 2 tests)
+        files=${files//,/ }
+        timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 120 --timeout-method thread \
+            -p no:cacheprovider > "$OUT/pytest.log" 2>&1
+        rc=$?
+        grep -E "passed|failed|error" "$OUT/pytest.log" | tail -3
+        [ $rc -ne 0 ] && { tail -30 "$OUT/pytest.log"; exit $rc; }
+        ;;
+    ab)
+        vs=$(field "$step" 2 "8,4")
+        for w in ${vs//,/ }; do
+            TDOA_PHAT1024_WAVES=$w timeout -k 10 240 python bench.py --steps ${STEPS:-400} --no-cpu \
+                $BENCH_ARGS > "$OUT/ab_$w.log" 2>&1 || { echo "bench $w failed"; tail -5 "$OUT/ab_$w.log"; exit 21; }
+            tail -1 "$OUT/ab_$w.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('WAVES=$w value %.4g kernel_ms %.4f frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))"
+        done
+        ;;
+    bench)
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
+        timeout -k 10 400 python bench.py --config $c --engine $e $BENCH_ARGS > "$OUT/bench_c${c}_$e.log" 2>&1 \
+            || { echo "bench failed"; tail -5 "$OUT/bench_c${c}_$e.log"; exit 22; }
+        tail -1 "$OUT/bench_c${c}_$e.log" > "$OUT/bench_c${c}_$e.json"
+        cut -c1-400 "$OUT/bench_c${c}_$e.json"
+        ;;
+    kstats)
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
+        PARGS="--config $c --engine $e --steps ${STEPS:-50} --warmup 3 --no-cpu $BENCH_ARGS"
+        prof "kt_c${c}_$e" --kernel-trace --stats || { echo "kstats failed"; tail -5 "$OUT/kt_c${c}_$e.log"; exit 23; }
+        cut -d, -f1-4,6 "$OUT/kt_c${c}_$e/run_kernel_stats.csv" | cut -c1-160 | head -6
+        ;;
+    pmc)
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
+        PARGS="--config $c --engine $e --steps 24 --warmup 2 --no-cpu $BENCH_ARGS"
+        prof "fetch_c${c}_$e" --pmc FETCH_SIZE || exit 24
+        prof "write_c${c}_$e" --pmc WRITE_SIZE || exit 25
+        echo "pmc c$c $e done"
+        ;;
+    sq)
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
+        PARGS="--config $c --engine $e --steps 24 --warmup 2 --no-cpu $BENCH_ARGS"
+        prof "sq1_c${c}_$e" --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU || exit 26
+        prof "sq2_c${c}_$e" --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU \
+            SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA || exit 27
+        echo "sq c$c $e done"
+        ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+            || { tail -20 "$OUT/smoke.log"; exit 28; }
+        tail -2 "$OUT/smoke.log"
+        ;;
+    *)
+        echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "run.sh done: $*"
