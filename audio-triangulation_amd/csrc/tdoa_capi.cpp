@@ -694,7 +694,7 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     const size_t sz = phat ? sizeof(float) : sizeof(int64_t);
     const size_t pk = (size_t)B * ctx->P * ctx->K * sz;
     const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
-    const bool fused_grid = phat && tdoa_gcc_phat_fused_grid(ctx->kp);
+    const bool fused_grid = phat ? tdoa_gcc_phat_fused_grid(ctx->kp) : tdoa_direct_fused_grid(ctx->kp);
     if (grid && !weighted && !fused_grid) {
         // the grid kernel reads the weighted scores back: keep them in scratch
         int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, pk, stream, "weighted-score");

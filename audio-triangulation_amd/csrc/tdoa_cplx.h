@@ -15,6 +15,32 @@
 
 namespace {
 
+#ifdef TDOA_NO_ASM
+// plain-C forms of the same primitives (the compiler schedules and pads them)
+__device__ __forceinline__ f2 c_addconj(f2 a, f2 b) { return f2{a.x + b.x, a.y - b.y}; }
+__device__ __forceinline__ f2 c_subconj(f2 a, f2 b) { return f2{a.x - b.x, a.y + b.y}; }
+__device__ __forceinline__ f2 c_add_mi(f2 a, f2 b) { return f2{a.x + b.y, a.y - b.x}; }
+__device__ __forceinline__ f2 c_add_i(f2 a, f2 b) { return f2{a.x - b.y, a.y + b.x}; }
+__device__ __forceinline__ f2 c_sub_mi(f2 a, f2 b) { return f2{a.y - b.y, b.x - a.x}; }
+__device__ __forceinline__ f2 c_sub_i(f2 a, f2 b) { return f2{b.y - a.y, a.x - b.x}; }
+__device__ __forceinline__ f2 c_conj_add_i(f2 a, f2 b) { return f2{a.x - b.y, -a.y - b.x}; }
+__device__ __forceinline__ f2 c_conj_add_mi(f2 a, f2 b) { return f2{a.x + b.y, b.x - a.y}; }
+__device__ __forceinline__ f2 c_mul(f2 a, f2 w) { return f2{a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x}; }
+__device__ __forceinline__ f2 c_mulconj(f2 a, f2 w) { return f2{a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y}; }
+__device__ __forceinline__ f2 c_conjmul(f2 a, f2 b) { return f2{a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x}; }
+__device__ __forceinline__ f2 c_mul_s(f2 a, f2 w) { return c_mul(a, w); }
+__device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w) { return c_mulconj(a, w); }
+__device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w) { const f2 r = c_mul(a, w); return f2{-r.x, -r.y}; }
+__device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w) { const f2 r = c_mulconj(a, w); return f2{-r.x, -r.y}; }
+__device__ __forceinline__ f2 c_mi(f2 x) { return f2{x.y, -x.x}; }
+__device__ __forceinline__ f2 c_i(f2 x) { return f2{-x.y, x.x}; }
+__device__ __forceinline__ f2 c_unit(f2 x, float e2)
+{
+    const float r = __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
+    return f2{x.x * r, x.y * r};
+}
+
+#else
 #define TDOA_PK(name, mnemonic, mods)                                      \
     __device__ __forceinline__ f2 name(f2 a, f2 b)                         \
     {                                                                      \
@@ -132,6 +158,8 @@ __device__ __forceinline__ f2 c_unit(f2 x, float e2)
     asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(f2{r, r}));
     return y;
 }
+
+#endif  // TDOA_NO_ASM
 
 // W_32^k = e^{-2 pi i k / 32}, k = 1..7 (the others by symmetry)
 __device__ __forceinline__ f2 w32c(int k)

@@ -101,7 +101,7 @@ __device__ __forceinline__ v4i_mf mf_limbs(const uint32_t (&w)[8], uint32_t sel)
     return r;
 }
 
-template <bool PREPARED>
+template <bool PREPARED, int TWC>
 __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
                                                       const int16_t *__restrict__ frames, int64_t B,
                                                       const int32_t *__restrict__ count, int n0, int nq,
@@ -196,6 +196,10 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
     }
     __syncthreads();
     argmax_prior_phase<int64_t>(kp, sm.scores, sm.best, out, f0, nf);
+    // grid solve (vga_heatmap.h:99-108) on the weighted scores still in LDS:
+    // no [B][P][K] round trip through HBM and no second launch
+    if (out.cell || out.xy || out.max_L)
+        grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf);
 }
 
 // --------------------------------------------------------------- EMA
@@ -381,6 +385,22 @@ static void direct_geometry(tdoa_kparams &kp, int &threads)
         threads = 1024;
 }
 
+static int direct_use_mfma()
+{
+    // matrix-core path (k_direct_mfma): TDOA_DIRECT_MFMA=0 keeps the VALU kernel (A/B)
+    static const int v = [] {
+        const char *s = getenv("TDOA_DIRECT_MFMA");
+        return s ? atoi(s) : 1;
+    }();
+    return v;
+}
+
+// the matrix-core kernel (config 2..4 shapes) runs the grid solve itself
+bool tdoa_direct_fused_grid(const tdoa_kparams &kp)
+{
+    return direct_use_mfma() && kp.N % 64 == 0 && kp.N >= 64 && kp.S <= 63;
+}
+
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
                        int64_t B, bool prepared, void *stream, int *lds_bytes_out,
                        const int32_t *count_dev)
@@ -389,12 +409,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
     tdoa_kparams kp = kp_in;
     int threads = 0;
-    // matrix-core path (k_direct_mfma): TDOA_DIRECT_MFMA=0 keeps the VALU kernel (A/B)
-    static const int use_mfma = [] {
-        const char *s = getenv("TDOA_DIRECT_MFMA");
-        return s ? atoi(s) : 1;
-    }();
-    if (use_mfma && kp.N % 64 == 0 && kp.N >= 64 && kp.S <= 63) {
+    if (tdoa_direct_fused_grid(kp)) {
         const int n0 = (kp.S + 15) / 16, nq = n0 + (kp.S + 1 + 15) / 16;  // lag columns -16 n0 .. 16 (nq - n0) - 1
         kp.PADW = MF_PADW;
         kp.RS = kp.N / 2 + 2 * MF_PADW;
@@ -410,12 +425,22 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         if (grid > INT_MAX)
             return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
         hipStream_t st = (hipStream_t)stream;
-        if (prepared)
-            hipLaunchKernelGGL((k_direct_mfma<true>), dim3((unsigned)grid), dim3(threads), lds, st, kp, out, frames,
-                               B, count_dev, n0, nq, (int)rsum_off);
-        else
-            hipLaunchKernelGGL((k_direct_mfma<false>), dim3((unsigned)grid), dim3(threads), lds, st, kp, out, frames,
-                               B, count_dev, n0, nq, (int)rsum_off);
+        constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
+#define TDOA_LAUNCH_MF(PREP, TWC)                                                                 \
+    hipLaunchKernelGGL((k_direct_mfma<PREP, TWC>), dim3((unsigned)grid), dim3(threads), lds, st, kp, \
+                       out, frames, B, count_dev, n0, nq, (int)rsum_off)
+        if (kp.TW == 1) {
+            if (prepared)
+                TDOA_LAUNCH_MF(true, 1);
+            else
+                TDOA_LAUNCH_MF(false, 1);
+        } else {
+            if (prepared)
+                TDOA_LAUNCH_MF(true, TWX);
+            else
+                TDOA_LAUNCH_MF(false, TWX);
+        }
+#undef TDOA_LAUNCH_MF
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : hip_fail(e, "k_direct_mfma launch");
     }

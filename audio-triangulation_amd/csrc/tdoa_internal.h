@@ -107,6 +107,8 @@ int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
                        const int16_t *frames, int64_t B, bool prepared,
                        void *stream, int *lds_bytes_out,
                        const int32_t *count_dev = nullptr);
+// the DIRECT launch for this shape also solves the grid (k_direct_mfma)
+bool tdoa_direct_fused_grid(const tdoa_kparams &kp);
 int tdoa_launch_heatmap(const tdoa_kparams &kp, const void *weighted, const void *max_L,
                         bool is_float, int64_t B, uint8_t *classes, void *stream);
 int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,

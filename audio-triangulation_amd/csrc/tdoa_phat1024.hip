@@ -117,6 +117,13 @@ __device__ __forceinline__ f2 unit(f2 x, float e2)
     return x * __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
 }
 
+// Lanes of a wave exchange data through LDS (the transposes, the grid score
+// table): a wave's DS instructions execute in issue order, but the compiler
+// models each lane as a separate thread and may reorder one lane's LDS write
+// and a later read it cannot prove aliasing.  This compiler-only barrier
+// (no instruction) pins the order of the wave's memory operations.
+__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_wave_barrier(); }
+
 struct Lane {
     int hw;           // half-wave of the wave
     int lane;         // 0..31 within the half-wave
@@ -182,6 +189,7 @@ template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *tile)
 {
     fft32p<INV, HALF_ZERO>(v);
+    wave_lds_order();  // after the previous pass's row reads of this tile
     const int wo = 8 * L.cs;
 #pragma unroll
     for (int k0 = 0; k0 < 32; k0 += 8) {
@@ -198,11 +206,13 @@ __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *ti
             sts_f2(tile, wo + P1K_ROW * slot(k), x);
         }
     }
+    wave_lds_order();  // before the row reads of other lanes' columns
 }
 template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, const f2 (&tw)[32])
 {
     fft32p<INV, HALF_ZERO>(v);
+    wave_lds_order();
     const int wo = 8 * L.cs;
 #pragma unroll
     for (int k = 0; k < 32; k++) {
@@ -211,6 +221,7 @@ __device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, 
             x = INV ? c_mulconj(x, tw[k]) : c_mul(x, tw[k]);
         sts_f2(tile, wo + P1K_ROW * slot(k), x);
     }
+    wave_lds_order();
 }
 // second half: row read (row res) + forward DFT-32 -> V[k2] = Z[res + 32 k2]
 __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 (&V)[33])
@@ -592,6 +603,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
             continue;
         }
         const bool paired = pbase >= 0;
+        wave_lds_order();
         float *wsc = (float *)wtiles;  // [P][KPAD][4]
 #pragma unroll
         for (int p = 0; p < P; p++)
@@ -605,6 +617,7 @@ __global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout
         if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
             *(float4 *)(wsc + (L.lane * P1K_KPAD + P1K_KPAD - 1) * 4) =
                 float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        wave_lds_order();
         float gv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
         int gu[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
         const char *ws = (const char *)wsc;
@@ -860,6 +873,21 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     const uint32_t *tups = (const uint32_t *)(prior + 128);
 
     const int tid = threadIdx.x, wave = tid >> 6, hw = (tid >> 5) & 1, lane64 = tid & 63;
+#ifdef TDOA_DIAG
+    // diagnostic build only: absolute s_memtime per phase of the first iteration
+    unsigned long long stamp[16] = {};
+    int nst = 0;
+#define LEAN_MARK()                                               \
+    do {                                                          \
+        if (nst < 16)                                             \
+            stamp[nst++] = __builtin_amdgcn_s_memtime();          \
+    } while (0)
+    stamp[nst++] = __builtin_amdgcn_s_memtime();
+#else
+#define LEAN_MARK() \
+    do {            \
+    } while (0)
+#endif
     Lane L;
     L.hw = hw;
     L.lane = tid & 31;
@@ -885,25 +913,57 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         for (int t = 0; t < 16; t++)
             w[t] = __builtin_nontemporal_load(row + 32 * t);
     };
+#ifdef LEAN_OLD_STAGING
+    uint32_t w0[16], w1[16];
     {
         const uint4 *src = (const uint4 *)kp.p1k_img;
         uint4 *dst = (uint4 *)twm;
         const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
-#pragma unroll 4
         for (int e = tid; e < n16; e += NT)
             dst[e] = src[e];
     }
     __syncthreads();
-
-    const float invL = 1.0f / 2048.0f;
-
-    const int64_t stride = (int64_t)gridDim.x * NF;
-    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += stride) {
-        const int64_t f = base + 2 * wave + hw;
-        const bool live = f < B;
-        uint32_t w0[16], w1[16], w2[16];
+    {
+        const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
         fetch(w0, f, 0);
         fetch(w1, f, 1);
+    }
+#else
+    // table image: its loads first (L2 hits), then the first frames' words
+    // (HBM), then the image's LDS writes -- the frames' latency overlaps the
+    // staging instead of following it
+    uint32_t w0[16], w1[16];
+    {
+        const uint4 *src = (const uint4 *)kp.p1k_img;
+        uint4 *dst = (uint4 *)twm;
+        const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
+        constexpr int SR = 4;  // image <= SR * NT * 16 B = 32 KiB (tdoa_phat1024_fits)
+        uint4 img[SR];
+#pragma unroll
+        for (int r = 0; r < SR; r++)
+            if (tid + r * NT < n16)
+                img[r] = src[tid + r * NT];
+        const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
+        fetch(w0, f, 0);
+        fetch(w1, f, 1);
+#pragma unroll
+        for (int r = 0; r < SR; r++)
+            if (tid + r * NT < n16)
+                dst[tid + r * NT] = img[r];
+    }
+    __syncthreads();
+
+#endif
+    const float invL = 1.0f / 2048.0f;
+
+    // one iteration per workgroup (grid = ceil(B / 16)): no value lives across
+    // a loop back-edge, which the register allocator answered with spills
+    {
+        const int64_t base = (int64_t)blockIdx.x * NF;
+        const int64_t f = base + 2 * wave + hw;
+        const bool live = f < B;
+        uint32_t w2[16];
+        LEAN_MARK();
         float wv[3][4];
         int best[3];
         auto finish_pair = [&](int p, f2 y0, f2 y31) {
@@ -946,7 +1006,9 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
 
         f2 U0[33], U1[33], y0, y31;
         lean_forward(L, w0, U0, e2);
+        LEAN_MARK();
         lean_forward(L, w1, U1, e2);
+        LEAN_MARK();
         {
             f2 v[32];
             lean_pretwiddle<true>(L, U0, U1, v);  // pair 0: (0, 1)
@@ -957,7 +1019,9 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             lean_row_inv(L, L.tileA, y0, y31);
         }
         finish_pair(0, y0, y31);
+        LEAN_MARK();
         lean_forward_cross(L, w2, U0, U1, e2);  // pairs 1: (0, 2), 2: (1, 2)
+        LEAN_MARK();
         {
             f2 v[32];
             lean_pretwiddle<false>(L, U0, U0, v);
@@ -965,6 +1029,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             lean_row_inv(L, L.tileA, y0, y31);
         }
         finish_pair(1, y0, y31);
+        LEAN_MARK();
         {
             f2 v[32];
             lean_pretwiddle<false>(L, U1, U1, v);
@@ -972,15 +1037,17 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             lean_row_inv(L, L.tileA, y0, y31);
         }
         finish_pair(2, y0, y31);
+        LEAN_MARK();
         if (live && L.lane == 0 && out.gate)
             out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
 
         if (!do_grid)
-            continue;
+            return;
         // ---- grid solve (vga_heatmap.h:99-108) of the wave's two frames:
         // weighted scores [p][KPAD] f2 (frame hw in component hw) in the wave's
         // tile space, lanes split the distinct lag tuples (4 consecutive per
         // lane and step, ascending: a strict '>' keeps the first maximum)
+        wave_lds_order();  // after the last pair's row reads of these tiles
         float *wsc = (float *)wtiles;  // [P][KPAD][2]
         const int gres = lane_res_sel(fresh_tid() & 31);
         const int gla = 2 * gres, glb = 2 * gres - 64;
@@ -994,26 +1061,34 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                     wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
         if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
             wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
+        wave_lds_order();  // the gathers read other lanes' score slots
         float gv[2] = {-INFINITY, -INFINITY};
         int gu[2] = {INT_MAX, INT_MAX};
         const char *ws = (const char *)wsc;
-        const uint4 *tq = (const uint4 *)tups;
-        uint4 q = tq[lane64];
+        // lane-strided: the 32 lanes of a gather read 32 consecutive tuples
+        // (first-cell order: neighbouring cells, so equal or adjacent lag slots
+        // -- broadcasts and distinct banks instead of 4-way conflicts)
+        uint32_t q[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            q[i] = tups[64 * i + lane64];
         for (int u0 = 0; u0 < Upad; u0 += 256) {
-            const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
             f2 Lg[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 // tuple fields are byte offsets of f2 slots in [p][KPAD]
-                const f2 l0 = lds_f2(ws, (int)(wq[i] & 0x3FFu));
-                const f2 l1 = lds_f2(ws, P1K_KPAD * 8 + (int)((wq[i] >> 10) & 0x3FFu));
-                const f2 l2 = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(wq[i] >> 20));
+                const f2 l0 = lds_f2(ws, (int)(q[i] & 0x3FFu));
+                const f2 l1 = lds_f2(ws, P1K_KPAD * 8 + (int)((q[i] >> 10) & 0x3FFu));
+                const f2 l2 = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(q[i] >> 20));
                 Lg[i] = (l0 + l1) + l2;
             }
-            q = tq[(u0 + 256 < Upad ? u0 + 256 : u0) / 4 + lane64];
+            const int un = u0 + 256 < Upad ? u0 + 256 : u0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                q[i] = tups[un + 64 * i + lane64];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int u = u0 + 4 * lane64 + i;
+                const int u = u0 + 64 * i + lane64;  // ascending per lane
                 if (Lg[i].x > gv[0]) {
                     gv[0] = Lg[i].x;
                     gu[0] = u;
@@ -1048,9 +1123,14 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                 }
             }
         }
-        // the tile space is rewritten by the next iteration's transposes:
-        // every lane's gathers must have landed (same wave: LDS ops in order)
+        LEAN_MARK();
     }
+#ifdef TDOA_DIAG
+    if (lane64 == 0 && (blockIdx.x * NW + wave) < 4096)
+        for (int i = 0; i < 16; i++)
+            g_diag_p1k[(blockIdx.x * NW + wave) * 16 + i] = stamp[i];
+#endif
+#undef LEAN_MARK
 }
 
 #ifdef TDOA_DIAG
@@ -1086,7 +1166,11 @@ int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
     constexpr int NF = 2 * NW;
     const int64_t groups = (B + NF - 1) / NF;
     const int64_t iters = (groups + c_resident - 1) / c_resident;
-    const int64_t grid = (groups + iters - 1) / iters;
+    // the one-wave kernel is persistent; the lean kernel does one group of
+    // 16 frames per workgroup
+    const int64_t grid = DUAL ? (groups + iters - 1) / iters : groups;
+    if (grid > 0x7FFFFFFF)
+        return tdoa_set_error(-1, "k_phat1024: batch too large for one launch");
     if constexpr (DUAL)
         hipLaunchKernelGGL((k_phat1024<NW, DUAL>), dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out,
                            frames, B, e2);

@@ -1,16 +1,74 @@
 """Frame sharding across GPUs (one process per GPU, torch.distributed).
 
-Frames are independent: a global batch splits into contiguous
-slices of ceil(B / world) frames, each rank localizes its slice on its own
-GPU, and only the small per-frame results (lags, gate, cell, xy: <= 24 B per
-frame) are gathered.  There is no data-path collective; RCCL carries only the
-result gather and timing reductions.
+Frames are independent: each rank owns its own frames -- a
+fixed per-rank batch (weak scaling, configs 2, 3, 5) or a contiguous slice of
+ceil(B / world) frames of one global batch (strong scaling, config 4's 1e6
+frames over 8 GPUs) -- and localizes them on its own GPU.  There is no
+data-path collective: RCCL carries only the timing barrier, the max-over-
+ranks of the elapsed time and (results / counts) reductions.
+
+bench.py's rank logic lives here so that the world-2 gloo test
+(tests/test_distributed.py) runs the same functions the driver's N-GPU runs
+execute: `init_distributed`, `frame_seed`, `rank_frames`, `timed`,
+`max_over_ranks`, `sum_over_ranks`, `ranks_seen`.
 """
 from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+@dataclass(frozen=True)
+class RankInfo:
+    rank: int
+    world: int
+    local_rank: int
+
+
+def rank_info() -> RankInfo:
+    """RANK / WORLD_SIZE / LOCAL_RANK of a torch.distributed.run launch (1 process otherwise)."""
+    return RankInfo(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                    int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def _active() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def init_distributed(backend: str = "nccl") -> RankInfo:
+    """Join the process group when launched with WORLD_SIZE > 1.  backend
+    "nccl" (RCCL on ROCm) binds the group to this rank's GPU; "gloo" is the
+    CPU rehearsal.  The rendezvous address defaults to 127.0.0.1."""
+    ri = rank_info()
+    if ri.world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", ri.local_rank))
+        else:
+            dist.init_process_group(backend)
+    return ri
+
+
+def finalize() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def ranks_seen() -> int:
+    """World size of the live process group (1 when not distributed)."""
+    return dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def frame_seed(base: int, rank: int, r: int = 0) -> int:
+    """Seed of rank `rank`'s r-th synthetic batch: every rank and every
+    rotating batch gets distinct frames."""
+    return int(base) + 7919 * int(rank) + 104729 * int(r)
 
 
 def shard_range(B: int, rank: int, world: int) -> tuple[int, int]:
@@ -20,18 +78,67 @@ def shard_range(B: int, rank: int, world: int) -> tuple[int, int]:
     return lo, min(B, lo + per)
 
 
+def rank_frames(batch: int, rank: int, world: int, scaling: str) -> int:
+    """Frames this rank processes per step: `batch` per rank ("weak") or its
+    shard_range slice of a global `batch` ("strong")."""
+    if scaling == "weak":
+        return int(batch)
+    lo, hi = shard_range(int(batch), rank, world)
+    return hi - lo
+
+
+def barrier() -> None:
+    if _active():
+        dist.barrier()
+
+
 def max_over_ranks(x: float, device=None) -> float:
     """Max of a scalar over all ranks (the bench's whole-job time)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active():
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
+def sum_over_ranks(xs, device=None) -> list[float]:
+    """Element-wise sum of a few scalars over all ranks (frame / trigger counts)."""
+    xs = [float(x) for x in xs]
+    if not _active():
+        return xs
+    t = torch.tensor(xs, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def timed(step, steps: int, warmup: int, sync=lambda: None, device=None,
+          on_start=None, on_end=None) -> dict:
+    """The bench contract's timed region: `warmup` untimed calls of step(k),
+    then EXACTLY `steps` calls bracketed by sync + barrier + sync on both
+    sides; the wall time is the max over ranks.  on_start / on_end run right
+    inside the bracket (e.g. HIP event records on the launch stream)."""
+    for k in range(warmup):
+        step(k)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    if on_start:
+        on_start()
+    for k in range(steps):
+        step(k)
+    if on_end:
+        on_end()
+    sync()
+    barrier()
+    sync()
+    wall = time.perf_counter() - t0
+    return {"wall_s": wall, "wall_max_s": max_over_ranks(wall, device)}
+
+
 def gather_results(local: dict, B: int) -> dict | None:
     """Concatenate every rank's per-frame numpy results in rank order on rank 0."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active():
         return local
     world = dist.get_world_size()
     parts = [None] * world

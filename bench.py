@@ -1,27 +1,37 @@
 #!/usr/bin/env python3
 """Headline benchmark: localizations/s on BASELINE config 2
-(3-mic triangle, 1024-sample int16 frames, batch 4096 per GPU, cross-correlation
--> argmax -> lag prior -> (x, y) grid solve), one process per GPU.
+(3-mic triangle, 1024-sample int16 frames, batch 4096 per GPU, GCC-PHAT
+cross-correlation -> argmax -> lag prior -> (x, y) grid solve), one process
+per GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--engine gcc_phat|direct]
+                    [--config 2|3|4|5]
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver, N > 1)
 
-A step = one fused libtdoa launch over one batch of 4096 frames already
-resident in HBM.  Batches rotate through > 256 MiB of frames so the Infinity
-Cache cannot serve them.  Frames are independent: each rank owns its own
-shard (weak scaling, no data-path collective; the only collectives are the
-timing barrier and the max-over-ranks of the elapsed time).
+A step = one libtdoa launch over one batch of frames already resident in HBM
+(config 5: one 512-sample hop of every stream).  Batches rotate through
+> 256 MiB of frames so the Infinity Cache cannot serve them.  Frames are
+independent: each rank owns its own frames (weak scaling for configs 2, 3, 5;
+config 4 splits one global batch of 1e6 frames, strong scaling) and there is
+no data-path collective -- the rank logic (seeds, shard sizes, the timed
+bracket with barrier + max-over-ranks) is tdoa/shard.py, which
+tests/test_distributed.py runs with gloo.
 
-Rank 0 prints one JSON line.  `roofline` prices the dominant kernel against
-HBM with ALGORITHMIC bytes (M*N*2 in + 4P lags + 8 xy = 6164 B/loc),
-`cpu_baseline` times the oracle (the reference's algorithm restated in C,
-OpenMP over frames) on a bounded sample of the same workload.
+Rank 0 prints one JSON line.  `roofline` prices the launch against HBM with
+ALGORITHMIC bytes (M*N*2 in + 4P lags + 8 xy per localization; 6164 B at
+config 2) over the launch's average duration from HIP events on the launch
+stream; `parity` reports, on the bench's own first batch, how often the
+GCC-PHAT lags / cells equal the DIRECT engine's (the reference's integer
+semantics) and the injected delays; `cpu_baseline` times the oracle (the
+reference's algorithm restated in C, OpenMP over frames) on a bounded sample
+of the same workload.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,26 +40,36 @@ sys.path.insert(0, os.path.join(ROOT, "audio-triangulation_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+from tdoa import shard  # noqa: E402
 
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak
 
-VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
-
-# BASELINE.json configs 2-4 (per-GPU batch; config 4's 1e6 frames are 125000 per GPU at 8)
+# BASELINE.json configs 2-5.  batch: per GPU (weak) or global (strong).
 CONFIGS = {
     2: dict(desc="BASELINE config 2: 3-mic triangle, 1024-sample frames", M=3, N=1024,
-            mics=None, batch=4096),
+            mics=None, batch=4096, scaling="weak"),
     3: dict(desc="BASELINE config 3: 4-mic square (0.15 m), 4096-sample frames, 6 pairs",
-            M=4, N=4096, mics="square", batch=65536),
-    4: dict(desc="BASELINE config 4: 8-mic circle (r 0.15 m), 2048-sample frames, 28 pairs",
-            M=8, N=2048, mics="circle", batch=125000),
+            M=4, N=4096, mics="square", batch=65536, scaling="weak"),
+    4: dict(desc="BASELINE config 4: 8-mic circle (r 0.15 m), 2048-sample frames, 28 pairs, "
+                 "global batch 1e6 split over the GPUs",
+            M=8, N=2048, mics="circle", batch=1_000_000, scaling="strong"),
     # batch = streams per GPU; one step = one 512-sample hop of every stream
     5: dict(desc="BASELINE config 5: streaming 48 kHz, 512-sample hop, 3-mic triangle, "
                  "trigger + DIRECT xcorr + EMA + grid, one hipGraph per hop",
-            M=3, N=1024, mics=None, batch=16384, fs=48000, hop=512),
+            M=3, N=1024, mics=None, batch=16384, fs=48000, hop=512, scaling="weak"),
 }
+
+
+def dominant_kernel(config: int, engine: str) -> str:
+    """Name of the kernel a config-2 launch runs (the one `traffic` was measured on)."""
+    if config == 2 and engine == "gcc_phat":
+        w = os.environ.get("TDOA_PHAT1024_WAVES", "8")
+        return {"8": "k_p1k_lean", "4": "k_phat1024"}.get(w, "k_gcc_phat_1024")
+    if config == 2:
+        return "k_direct_mfma" if os.environ.get("TDOA_DIRECT_MFMA", "1") != "0" else "k_direct"
+    return ""
 
 
 def phat_flops(M, N):
@@ -63,16 +83,18 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None,
-                    help="default 400 (config 2), 200 (config 5), 20 otherwise")
+                    help="default 400 (config 2), 200 (config 5), 5 (config 4), 20 otherwise")
     ap.add_argument("--warmup", type=int, default=None,
-                    help="default 20 (config 2, 5), 3 otherwise")
+                    help="default 20 (config 2, 5), 2 (config 4), 3 otherwise")
     ap.add_argument("--engine", default="gcc_phat", choices=["gcc_phat", "direct"])
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per GPU (weak) / in total (strong); default: the config's")
     ap.add_argument("--rotate-mib", type=int, default=320,
                     help="frames rotated per rank (> 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--also", action="store_true", help="also time the other engine")
     ap.add_argument("--no-grid", action="store_true", help="diagnostic: skip the grid solve")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
@@ -81,9 +103,9 @@ def parse():
     if a.batch is None:
         a.batch = cfg["batch"]
     if a.steps is None:
-        a.steps = {2: 400, 5: 200}.get(a.config, 20)
+        a.steps = {2: 400, 5: 200, 4: 5}.get(a.config, 20)
     if a.warmup is None:
-        a.warmup = 20 if a.config in (2, 5) else 3
+        a.warmup = {2: 20, 5: 20, 4: 2}.get(a.config, 3)
     if a.config == 5:
         a.engine = "direct"  # the streaming loop runs the reference's DIRECT path
     return a
@@ -98,70 +120,101 @@ def config_mics(cfg):
     return None
 
 
-def time_engine(engine, args, dev, rank, world, lut_cache):
+def make_frames(B, M, N, lut, S, seed, dev, chunk=65536):
+    """Synthetic ADC frames generated on the device in chunks (bounded temporaries)."""
     from tdoa import synth
+    if B <= chunk:
+        fr, _, tau = synth.adc_frames(B, M, N, lut, S, seed, device=dev)
+        return fr, tau
+    fr = torch.empty((B, M, N), dtype=torch.int16, device=dev)
+    tau = torch.empty((B, M), dtype=torch.int64, device=dev)
+    for i, lo in enumerate(range(0, B, chunk)):
+        hi = min(B, lo + chunk)
+        f, _, t = synth.adc_frames(hi - lo, M, N, lut, S, seed + 31 * i, device=dev)
+        fr[lo:hi], tau[lo:hi] = f, t
+    return fr, tau
+
+
+def parity_report(engine, loc, frames, tau, out):
+    """Agreement of this run's outputs on its first batch with the DIRECT
+    engine (the reference's integer semantics, correlations.c:20-23) and with
+    the injected integer delays.  Outside the timed region."""
+    from tdoa.localizer import Localizer
+    B = frames.shape[0]
+    P = loc.dims.P
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    rep = {"frames": int(B), "sample": "the bench's first batch on rank 0 (first 65536 frames)"}
+    # injected delays: pair (0, m) lag = tau_m (synth.adc_frames)
+    t = tau.cpu().numpy()
+    M = loc.dims.M
+    rep["lags_equal_injected_pairs0m"] = float((got["lags"][:, :M - 1] == t[:, 1:]).mean())
+    if engine == "gcc_phat":
+        d = Localizer(engine="direct", num_mics=M, frame_len=loc.dims.N,
+                      mic_xy=None if M == 3 else loc.mics(), device=loc.device)
+        dref = {k: v.cpu().numpy() for k, v in d.localize(frames).items()}
+        d.close()
+        same = got["lags"] == dref["lags"]
+        rep["lags_equal_direct"] = float(same.mean())
+        rep["frames_all_lags_equal_direct"] = float(same.all(-1).mean())
+        if "cell" in got:
+            rep["cells_equal_direct"] = float((got["cell"] == dref["cell"]).mean())
+        rep["contract"] = ("lags equal DIRECT wherever the fp64 GCC-PHAT top-2 margin exceeds "
+                           "2e-4 (tests/test_gpu_gcc_phat.py); DIRECT is bit-exact with the oracle")
+    else:
+        rep["contract"] = "DIRECT is bit-exact with the oracle (tests/test_gpu_parity.py)"
+    rep["pairs"] = int(P)
+    return rep
+
+
+def time_engine(engine, args, dev, ri, cache):
     from tdoa.localizer import Localizer
     cfg = CONFIGS[args.config]
     loc = Localizer(engine=engine, num_mics=cfg["M"], frame_len=cfg["N"], mic_xy=config_mics(cfg),
                     device=dev.index)
     M, N, P = loc.dims.M, loc.dims.N, loc.dims.P
-    B = args.batch
-    lut = loc.lut().reshape(P, 101, 101)
-    lut_cache["lut"], lut_cache["window"] = lut, loc.window()
+    B = shard.rank_frames(args.batch, ri.rank, ri.world, cfg["scaling"])
+    lut = loc.lut().reshape(P, -1)
+    cache["lut"], cache["window"] = lut, loc.window()
     per_batch = B * M * N * 2
     R = max(1, -(-args.rotate_mib * (1 << 20) // per_batch))
-    batches = []
+    batches, taus = [], []
     for r in range(R):
-        fr, _, _ = synth.adc_frames(B, M, N, lut, loc.dims.S,
-                                    synth.SEEDS[args.config] + 7919 * rank + 104729 * r,
-                                    device=dev)
+        fr, tau = make_frames(B, M, N, lut, loc.dims.S,
+                              shard.frame_seed(0x5EED0000 + args.config, ri.rank, r), dev)
         batches.append(fr)
+        taus.append(tau)
     out = loc.alloc_outputs(B, grid=not args.no_grid)
     stream = torch.cuda.current_stream(dev)
-    for k in range(args.warmup):
-        loc.localize_into(batches[k % R], out, stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        loc.localize_into(batches[k % R], out, stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)  # GPU time of the K launches on the launch stream
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
-    total = world * B * args.steps
+    t = shard.timed(lambda k: loc.localize_into(batches[k % R], out, stream), args.steps,
+                    args.warmup, sync=lambda: torch.cuda.synchronize(dev), device=dev,
+                    on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # GPU time per launch, launch stream
+    total = shard.sum_over_ranks([B * args.steps], device=dev)[0]
     bytes_per_loc = M * N * 2 + 4 * P + 8
-    kern_s = ev_ms / 1e3 / args.steps
     res = {
         "engine": engine,
-        "value": total / wall_max,
-        "ms_per_step": wall_max * 1e3 / args.steps,
+        "value": total / t["wall_max_s"],
+        "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
         "kernel_ms": kern_s * 1e3,
+        "frames_per_rank": B,
         "bytes_per_loc": bytes_per_loc,
         "achieved_gbs": bytes_per_loc * B / kern_s / 1e9,
         "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
         "rotate_batches": R,
     }
-    # sanity: outputs of the last step are finite / in range
     lags = out["lags"].cpu()
     assert int(lags.abs().max()) <= loc.dims.S
+    if ri.rank == 0 and not args.no_parity:
+        n = min(B, 65536)
+        f0 = batches[0][:n].contiguous()
+        res["parity"] = parity_report(engine, loc, f0, taus[0][:n], loc.localize(f0))
     loc.close()
     return res
 
 
-def time_stream(args, dev, rank, world, cache):
+def time_stream(args, dev, ri, cache):
     """Config 5: S streams per GPU, capture ring resident in HBM (64 hops per
     stream, replayed cyclically); a step = one hop of every stream."""
     from tdoa import synth
@@ -173,53 +226,87 @@ def time_stream(args, dev, rank, world, cache):
     lut = loc.lut()
     cache["lut"], cache["window"], cache["S"] = lut, loc.window(), loc.dims.S
     T = 64 * H
-    cap = synth.adc_stream(S, T, 3, lut, loc.dims.S, synth.SEEDS[5] + 7919 * rank, device=dev)
+    cap = synth.adc_stream(S, T, 3, lut, loc.dims.S, shard.frame_seed(synth.SEEDS[5], ri.rank),
+                           device=dev)
     torch.cuda.synchronize(dev)
     pipe = StreamPipeline(loc, cap, hop=H, use_graph=True)
     st = pipe.stream
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     for _ in range(args.warmup):
         pipe.step()
     st.synchronize()
     _, trig0, gated0 = pipe.totals()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(st)
-    for _ in range(args.steps):
-        pipe.step()
-    ev1.record(st)
-    st.synchronize()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
+    t = shard.timed(lambda k: pipe.step(), args.steps, 0,
+                    sync=lambda: (st.synchronize(), torch.cuda.synchronize(dev)), device=dev,
+                    on_start=lambda: ev0.record(st), on_end=lambda: ev1.record(st))
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     _, trig1, gated1 = pipe.totals()
-    t = torch.tensor([wall, trig1 - trig0, gated1 - gated0], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = t[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t[0] = mx[0]
-    wall_max, trig, gated = float(t[0]), float(t[1]), float(t[2])
-    samples = world * S * H * args.steps
+    trig, gated = shard.sum_over_ranks([trig1 - trig0, gated1 - gated0], device=dev)
+    # per-hop latency, outside the timed region: one hop in flight at a time,
+    # submit -> the hop's records readable on the host (graph replay + kernels
+    # + the count read-back), and the hop's GPU time from events around it
+    lat_host, lat_gpu = [], []
+    e_a = torch.cuda.Event(enable_timing=True)
+    e_b = torch.cuda.Event(enable_timing=True)
+    for _ in range(min(200, max(50, args.steps))):
+        t0 = time.perf_counter()
+        e_a.record(st)
+        pipe.step()
+        e_b.record(st)
+        st.synchronize()
+        lat_host.append(time.perf_counter() - t0)
+        lat_gpu.append(e_a.elapsed_time(e_b) / 1e3)
+    samples = ri.world * S * H * args.steps
     pipe.close()
-    return {"engine": "direct", "value": trig / wall_max, "ms_per_step": wall_max * 1e3 / args.steps,
+    pct = lambda a, q: float(np.percentile(np.asarray(a) * 1e3, q))  # noqa: E731
+    return {"engine": "direct", "value": trig / t["wall_max_s"],
+            "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
             "kernel_ms": gpu_s * 1e3 / args.steps, "triggered": trig, "gated": gated,
-            "stream_samples_per_s": samples / wall_max,
-            "realtime_streams": samples / wall_max / cfg["fs"],
-            "capture_bytes_per_step": world * S * H * 3}
+            "stream_samples_per_s": samples / t["wall_max_s"],
+            "realtime_streams": samples / t["wall_max_s"] / cfg["fs"],
+            "capture_bytes_per_step": ri.world * S * H * 3,
+            "latency_ms": {"p50": pct(lat_host, 50), "p99": pct(lat_host, 99),
+                           "gpu_p50": pct(lat_gpu, 50), "gpu_p99": pct(lat_gpu, 99),
+                           "hops": len(lat_host),
+                           "kind": "per hop, one hop in flight: submit -> results on the host "
+                                   "(p50/p99), and the hop's GPU time from events (gpu_*); "
+                                   "measured after the timed region"}}
+
+
+def _cpu_info(threads):
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return {"cores": threads, "nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
+            "threads_source": "OMP_NUM_THREADS (the box's CPU share per GPU)"
+            if os.environ.get("OMP_NUM_THREADS") else "all CPUs in this process's affinity set"}
+
+
+def _cpu_threads():
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline_stream(args, lut, window, S_lag):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from tdoa import synth
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     adc = synth.adc_stream(64, 64 * 512, 3, lut, S_lag, synth.SEEDS[5]).numpy()
     O.stream_run(adc[:4, :4096], 1024, 48000, S_lag, window, lut, threads=threads)
     n, t0 = 0, time.perf_counter()
@@ -227,7 +314,7 @@ def cpu_baseline_stream(args, lut, window, S_lag):
         r = O.stream_run(adc, 1024, 48000, S_lag, window, lut, threads=threads, max_trig=64)
         n += int(r["n_trig"].sum())
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "localizations/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "localizations/s", **_cpu_info(threads), "kind": "port",
             "sample": f"{n} triggered frames from 64 streams x 32768 samples (config-5 capture "
                       f"bytes) in {dt:.1f} s, oracle orc_stream_run (sample_compute.h:53-146 "
                       f"sample by sample: rings, trigger, DIRECT xcorr, EMA, grid), OpenMP "
@@ -240,7 +327,7 @@ def cpu_baseline(args, lut, window):
     from tdoa import synth
     cfg = CONFIGS[args.config]
     M, N = cfg["M"], cfg["N"]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     nfr = 2048 if args.config == 2 else 128
     fr, _, _ = synth.adc_frames(nfr, M, N, lut, 46, synth.SEEDS[args.config])
     fr = fr.numpy()
@@ -250,41 +337,49 @@ def cpu_baseline(args, lut, window):
         O.localize_batch(fr, 46, window, lut, threads=threads, want_scores=False)
         n += fr.shape[0]
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "localizations/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "localizations/s", **_cpu_info(threads), "kind": "port",
             "sample": f"{n} config-{args.config} frames ({M}x{N} ADC-like, batches of {nfr}) "
-                      f"in {dt:.1f} s, "
-                      f"oracle/tdoa_oracle.c (reference correlations.c + vga_heatmap.h "
-                      f"algorithm, DIRECT integer xcorr), OpenMP {threads} threads"}
+                      f"in {dt:.1f} s, oracle/tdoa_oracle.c (reference correlations.c + "
+                      f"vga_heatmap.h algorithm, DIRECT integer xcorr), OpenMP {threads} threads"}
+
+
+def traffic_entry(args):
+    """HBM bytes per launch from the committed PMC passes, used only when they
+    were taken on the kernel this run dispatches."""
+    kname = dominant_kernel(args.config, args.engine)
+    if not kname or not os.path.exists(args.traffic_json):
+        return None, None
+    try:
+        tj = json.load(open(args.traffic_json))
+    except (OSError, ValueError):
+        return None, None
+    e = tj.get(f"c{args.config}_{args.engine}") or {}
+    if e.get("kernel") != kname:
+        return None, None
+    src = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+           f"passes on {kname} ({e.get('date', 'undated')}), read = 2 x FETCH_SIZE")
+    return e.get("hbm_bytes_per_launch"), src
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    ri = shard.init_distributed("nccl")
+    dev = torch.device("cuda", ri.local_rank)
     torch.cuda.set_device(dev)
     cache = {}
     if args.config == 5:
-        return main_stream(args, dev, rank, world, cache)
-    main_res = time_engine(args.engine, args, dev, rank, world, cache)
+        return main_stream(args, dev, ri, cache)
+    main_res = time_engine(args.engine, args, dev, ri, cache)
     other = None
     if args.also:
         other = time_engine("direct" if args.engine == "gcc_phat" else "gcc_phat", args, dev,
-                            rank, world, cache)
-    if rank == 0:
-        traffic = None
-        if args.config == 2 and os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                traffic = tj.get(args.engine, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+                            ri, cache)
+    world = shard.ranks_seen()
+    if ri.rank == 0:
+        traffic, tsrc = traffic_entry(args)
         cfg = CONFIGS[args.config]
         shape = f"{cfg['M']}-mic x {cfg['N']}-sample frames"
+        B = main_res["frames_per_rank"]
         line = {
             "metric": f"GCC-PHAT localizations/sec, {shape}"
             if args.engine == "gcc_phat" else
@@ -292,24 +387,31 @@ def main():
             "value": main_res["value"],
             "unit": "localizations/s",
             "n_gpus": world,
+            "ranks_seen": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": cfg["scaling"],
             "vs_baseline": None,
             "dtype": "f32" if args.engine == "gcc_phat" else "int16->int64",
-            "data": "synthetic (ADC-like u8 frames, injected integer delays, resident in HBM, "
-                    f"{main_res['rotate_batches']} rotating batches > 256 MiB)",
-            "config": {"workload": f"{cfg['desc']}, batch {args.batch} per GPU, "
+            "data": "synthetic (ADC-like u8 frames, injected integer delays, generated on the GPU, "
+                    f"resident in HBM, {main_res['rotate_batches']} rotating batches > 256 MiB)"
+                    if main_res["rotate_batches"] > 1 else
+                    "synthetic (ADC-like u8 frames, injected integer delays, generated on the GPU, "
+                    "resident in HBM; one batch larger than the 256 MiB Infinity Cache)",
+            "config": {"workload": f"{cfg['desc']}, {B} frames per GPU per step, "
                                    "xcorr + lag prior + (x,y) grid",
-                       "engine": args.engine, "batch_per_gpu": args.batch, "mics": cfg["M"],
-                       "frame_len": cfg["N"],
+                       "engine": args.engine, "batch_per_gpu": B,
+                       "global_batch": args.batch if cfg["scaling"] == "strong" else B * world,
+                       "mics": cfg["M"], "frame_len": cfg["N"],
                        "parallelism": f"dp{world} (frame shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": main_res["achieved_gbs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": main_res["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic": traffic,
+                         "traffic_source": tsrc,
+                         "kernel": dominant_kernel(args.config, args.engine) or "all kernels of a launch",
                          "kernel_ms": main_res["kernel_ms"],
                          "bytes_per_loc": main_res["bytes_per_loc"]},
             # the bound that actually binds an fp32 FFT path: FP32 vector issue
@@ -317,26 +419,28 @@ def main():
                               "unit": "TFLOP/s", "frac": main_res["valu_tflops"] / VALU_PEAK_TFLOPS,
                               "flop_model": "SURVEY.md 8(d) GCC-PHAT model"}
             if args.engine == "gcc_phat" else None,
+            "parity": main_res.get("parity"),
             "cpu_baseline": None,
         }
         if other is not None:
+            other.pop("parity", None)
             line["other_engine"] = other
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args, cache["lut"], cache["window"])
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    shard.finalize()
 
 
-def main_stream(args, dev, rank, world, cache):
-    res = time_stream(args, dev, rank, world, cache)
-    if rank == 0:
+def main_stream(args, dev, ri, cache):
+    res = time_stream(args, dev, ri, cache)
+    world = shard.ranks_seen()
+    if ri.rank == 0:
         cfg = CONFIGS[5]
         line = {
             "metric": "streaming localizations/sec (triggered frames), 3-mic x 1024-sample "
                       "frames, 48 kHz, 512-sample hop",
             "value": res["value"], "unit": "localizations/s", "n_gpus": world,
+            "ranks_seen": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int16->int64",
@@ -348,6 +452,7 @@ def main_stream(args, dev, rank, world, cache):
                        "parallelism": f"dp{world} (stream shards, no collective)"},
             "stream": {k: res[k] for k in ("kernel_ms", "triggered", "gated",
                                            "stream_samples_per_s", "realtime_streams")},
+            "latency_ms": res["latency_ms"],
             "roofline": None,
             "cpu_baseline": None,
         }
@@ -355,9 +460,7 @@ def main_stream(args, dev, rank, world, cache):
             line["cpu_baseline"] = cpu_baseline_stream(args, cache["lut"], cache["window"],
                                                        cache["S"])
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    shard.finalize()
 
 
 if __name__ == "__main__":

@@ -1,8 +1,11 @@
-"""World-size-2 gloo rehearsal of the multi-GPU path on CPU: each rank
-localizes its contiguous frame shard (here with the oracle, as no GPU is
-present) and rank 0 gathers; the gathered results must equal the
-single-process run frame for frame.  Also checks the max-over-ranks timing
-reduction bench.py uses."""
+"""World-size-2 gloo rehearsal of the multi-GPU path on CPU.
+
+bench.py's rank logic lives in tdoa/shard.py; the workers below run those
+same functions -- init_distributed (from RANK / WORLD_SIZE / LOCAL_RANK),
+frame_seed, rank_frames with bench.CONFIGS' scaling, the timed bracket
+(barrier + max over ranks), sum_over_ranks and ranks_seen -- with the
+oracle as the injected compute (no GPU here).  The gathered per-frame
+results must equal the single-process run frame for frame."""
 import os
 import socket
 
@@ -24,29 +27,46 @@ def _free_port():
 
 def _worker(rank, world, port, q):
     import sys
-    for p in (PKG, os.path.join(ROOT, "oracle")):
+    for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    import oracle as O
+    from tdoa import shard
+    ri = shard.init_distributed("gloo")
     try:
-        import oracle as O
-        from tdoa import shard
         g = np.load(os.path.join(GOLDEN, "pipeline_cfg2.npz"))
         win = np.load(os.path.join(GOLDEN, "window_q15.npz"))["n1024"]
         frames, lut = g["frames"][:45], g["lut"]  # 45: ragged split 23 + 22
         res = shard.localize_sharded(frames, lambda f: O.localize_batch(f, 46, win, lut))
-        t = shard.max_over_ranks(float(rank + 1))
+        # the bench's timed bracket with an injected CPU step: every rank's own
+        # shard, the wall time max-reduced, the frame count sum-reduced
+        lo, hi = shard.shard_range(45, ri.rank, ri.world)
+        done = []
+        t = shard.timed(lambda k: done.append(O.localize_batch(frames[lo:hi], 46, win, lut)),
+                        steps=3, warmup=1)
+        total = shard.sum_over_ranks([(hi - lo) * 3])[0]
+        mx = shard.max_over_ranks(float(rank + 1))
+        cfg4 = bench.CONFIGS[4]
+        per4 = shard.rank_frames(cfg4["batch"], ri.rank, ri.world, cfg4["scaling"])
+        per2 = shard.rank_frames(bench.CONFIGS[2]["batch"], ri.rank, ri.world,
+                                 bench.CONFIGS[2]["scaling"])
+        seeds = [shard.frame_seed(0x5EED0002, ri.rank, r) for r in range(3)]
+        out = {"rank": rank, "ranks_seen": shard.ranks_seen(), "wall": t["wall_s"],
+               "wall_max": t["wall_max_s"], "steps_done": len(done), "total": total, "max": mx,
+               "per4": per4, "per2": per2, "seeds": seeds}
         if rank == 0:
             full = O.localize_batch(frames, 46, win, lut)
-            ok = all((res[k] == full[k]).all() for k in ("lags", "gate", "cell", "xy"))
-            q.put((ok, t, shard.shard_range(45, 0, world), shard.shard_range(45, 1, world)))
+            out["ok"] = all((res[k] == full[k]).all() for k in ("lags", "gate", "cell", "xy"))
+        q.put(out)
         dist.barrier()
     finally:
-        dist.destroy_process_group()
+        shard.finalize() if dist.is_initialized() else None
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_shards_match_single_process():
+def test_two_rank_gloo_bench_rank_logic():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -56,10 +76,17 @@ def test_two_rank_gloo_shards_match_single_process():
     for p in procs:
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    ok, t, r0, r1 = q.get(timeout=5)
-    assert ok
-    assert t == 2.0
-    assert r0 == (0, 23) and r1 == (23, 45)
+    rs = sorted([q.get(timeout=5) for _ in range(2)], key=lambda r: r["rank"])
+    assert rs[0]["ok"]
+    assert all(r["ranks_seen"] == 2 for r in rs)
+    assert all(r["steps_done"] == 3 + 1 for r in rs)           # warmup 1 + exactly 3 timed
+    assert all(r["total"] == 45 * 3 for r in rs)               # every frame counted once
+    wall_max = max(r["wall"] for r in rs)
+    assert all(abs(r["wall_max"] - wall_max) < 1e-12 for r in rs)
+    assert all(r["max"] == 2.0 for r in rs)
+    assert rs[0]["per4"] + rs[1]["per4"] == 1_000_000           # config 4: one global batch
+    assert rs[0]["per2"] == rs[1]["per2"] == 4096               # config 2: per-GPU batch
+    assert len(set(rs[0]["seeds"] + rs[1]["seeds"])) == 6       # distinct frames per rank/batch
 
 
 def test_shard_range_covers_everything_once():
@@ -71,3 +98,12 @@ def test_shard_range_covers_everything_once():
                 lo, hi = shard_range(B, r, world)
                 cover[lo:hi] += 1
             assert (cover == 1).all()
+
+
+def test_single_process_defaults():
+    from tdoa import shard
+    os.environ.pop("WORLD_SIZE", None)
+    ri = shard.init_distributed("gloo")
+    assert (ri.rank, ri.world) == (0, 1) and shard.ranks_seen() == 1
+    assert shard.max_over_ranks(3.5) == 3.5 and shard.sum_over_ranks([2, 3]) == [2.0, 3.0]
+    assert shard.rank_frames(10, 0, 1, "strong") == 10

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Timeline of k_p1k_lean (libtdoa_diag.so: absolute s_memtime stamps per wave
+at its phase boundaries).  Diagnostic only; never used by tests or bench.py.
+
+    python tools/diag_lean.py [B]
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("TDOA_LIB", os.path.join(ROOT, "audio-triangulation_amd", "tdoa", "libtdoa_diag.so"))
+sys.path.insert(0, os.path.join(ROOT, "audio-triangulation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import tdoa  # noqa: E402
+from tdoa import synth  # noqa: E402
+from tdoa.localizer import Localizer  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+loc = Localizer(engine="gcc_phat")
+fr, _, _ = synth.adc_frames(B, 3, 1024, loc.lut(), 46, 1, device="cuda")
+out = loc.alloc_outputs(B)
+for _ in range(20):
+    loc.localize_into(fr, out)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+loc.localize_into(fr, out)
+e1.record()
+torch.cuda.synchronize()
+L = tdoa.load()
+L.tdoa_diag_fetch_p1k.argtypes = [C.c_void_p, C.c_int]
+buf = np.zeros(1 << 16, np.uint64)
+assert L.tdoa_diag_fetch_p1k(buf.ctypes.data_as(C.c_void_p), 1 << 16) == 0
+st = buf.reshape(-1, 16).astype(np.int64)
+st = st[st[:, 0] > 0]
+names = ["start", "staged", "mic0", "mic1", "pair01", "mic2+cross", "pair02", "pair12", "grid"]
+n = len(names)
+t = st[:, :n] - st[:, 0].min()
+print(f"B={B} waves={len(st)} kernel {e0.elapsed_time(e1) * 1e3:.1f} us (event, one launch)")
+print("absolute (cycles from the first wave's start): p0 / p50 / p90 / max")
+for i, nm in enumerate(names):
+    c = t[:, i]
+    print(f"  {nm:11s} {c.min():8d} {np.median(c):8.0f} {np.percentile(c, 90):8.0f} {c.max():8d}")
+print("phase durations: p10 / p50 / p90")
+for i in range(1, n):
+    d = t[:, i] - t[:, i - 1]
+    print(f"  {names[i]:11s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")

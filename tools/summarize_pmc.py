@@ -1,52 +1,65 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 PMC CSVs into profiles/hbm_traffic.json (per-launch HBM
-bytes of the dominant kernel of each engine).
+"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/gpu/run.sh pmc:C:E)
+into profiles/hbm_traffic.json: per-launch HBM bytes of each kernel a config
+/ engine launch dispatches, keyed "c<config>_<engine>".
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports
 half the bytes of a wide (16 B/lane) coalesced streaming read, so read bytes
-= 2 * FETCH_SIZE KiB; WRITE_SIZE is exact for 16-B stores (our outputs are
-4-8 B/lane stores: uncalibrated, small).  FETCH_SIZE and WRITE_SIZE come from
-separate --pmc passes.
+= 2 * FETCH_SIZE KiB; WRITE_SIZE is exact for 16-B stores (4-8 B stores:
+uncalibrated, small).  FETCH_SIZE and WRITE_SIZE come from separate passes.
 
-    python tools/summarize_pmc.py gpurun_out/pmc profiles/hbm_traffic.json
+    python tools/summarize_pmc.py <pmc-dir> <config> <engine> <dominant-kernel> \
+        <algorithmic-bytes-per-launch> [profiles/hbm_traffic.json]
 """
 import csv
+import datetime
 import json
 import os
 import sys
+from collections import defaultdict
 
-KERNELS = {"gcc_phat": "k_phat1024", "direct": "k_direct"}
 
-
-def per_dispatch(path, counter, kname):
-    vals = []
+def per_kernel(path, counter):
+    """{kernel name: [value per dispatch]} (warm-up quarter dropped)."""
+    vals = defaultdict(list)
     if not os.path.exists(path):
-        return vals
+        return {}
     for r in csv.DictReader(open(path)):
-        if kname in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals.append(float(r["Counter_Value"]))
-    return vals
+        if r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            vals[name].append(float(r["Counter_Value"]))
+    return {k: v[len(v) // 4:] for k, v in vals.items() if v[len(v) // 4:]}
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    out = {"note": "per launch of 4096 cfg2 frames; read = 2 x FETCH_SIZE KiB (gfx950 wide-load "
-                   "correction), write = WRITE_SIZE KiB; algorithmic bytes = 4096 x 6164"}
-    for eng, kn in KERNELS.items():
-        f = per_dispatch(os.path.join(src, f"fetch_{eng}", "run_counter_collection.csv"), "FETCH_SIZE", kn)
-        w = per_dispatch(os.path.join(src, f"write_{eng}", "run_counter_collection.csv"), "WRITE_SIZE", kn)
-        if not f:
-            continue
-        f = f[len(f) // 4:]  # drop warm-up dispatches
-        w = w[len(w) // 4:] if w else [0.0]
-        rd = 2.0 * 1024.0 * sum(f) / len(f)
-        wr = 1024.0 * sum(w) / len(w)
-        out[eng] = {"fetch_size_kib": sum(f) / len(f), "write_size_kib": sum(w) / len(w),
-                    "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-                    "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": 4096 * 6164,
-                    "dispatches": len(f)}
+    src, cfg, eng, dom, algo = sys.argv[1:6]
+    dst = sys.argv[6] if len(sys.argv) > 6 else "profiles/hbm_traffic.json"
+    f = per_kernel(os.path.join(src, f"fetch_c{cfg}_{eng}", "run_counter_collection.csv"), "FETCH_SIZE")
+    w = per_kernel(os.path.join(src, f"write_c{cfg}_{eng}", "run_counter_collection.csv"), "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(f) | set(w)):
+        if k.startswith("at::") or "native" in k:
+            continue  # torch's own kernels (synthetic data generation)
+        rd = 2.0 * 1024.0 * (sum(f.get(k, [0])) / max(1, len(f.get(k, []))))
+        wr = 1024.0 * (sum(w.get(k, [0])) / max(1, len(w.get(k, []))))
+        kernels[k] = {"hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes": rd + wr,
+                      "dispatches": len(f.get(k, []))}
+    total = sum(v["hbm_bytes"] for k, v in kernels.items() if v["dispatches"])
+    dk = next((v for k, v in kernels.items() if dom in k), None)
+    out = json.load(open(dst)) if os.path.exists(dst) else {}
+    out["note"] = ("per launch; read = 2 x FETCH_SIZE KiB (gfx950 wide-load correction), write = "
+                   "WRITE_SIZE KiB; separate --pmc passes; algorithmic = frames x (M N 2 + 4P + 8)")
+    out[f"c{cfg}_{eng}"] = {
+        "kernel": dom,
+        "date": datetime.date.today().isoformat(),
+        "hbm_bytes_per_launch": dk["hbm_bytes"] if dk else None,
+        "hbm_bytes_all_kernels_per_launch": total,
+        "algorithmic_bytes_per_launch": float(algo),
+        "ratio_to_algorithmic": (dk["hbm_bytes"] / float(algo)) if dk else None,
+        "kernels": kernels,
+    }
     json.dump(out, open(dst, "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    print(json.dumps(out[f"c{cfg}_{eng}"], indent=1))
 
 
 if __name__ == "__main__":
