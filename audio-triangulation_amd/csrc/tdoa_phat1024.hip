@@ -707,8 +707,13 @@ namespace {
 
 // front end + forward FFT_1024 of one mic row, then the partner swap: V[k],
 // V[31 - k] hold Z[b], Z[N - b] (paired layout); V[32] = unit X[512] (lane 0)
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+template <typename Hook = NoHook>
 __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)[16], f2 (&V)[33],
-                                              float e2)
+                                              float e2, Hook after_front = Hook())
 {
     f2 v[32];
     {
@@ -728,6 +733,7 @@ __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)
             v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
         }
     }
+    after_front();  // the row's words are consumed
     fft_col_lds<false, true>(L, v, L.tileA);
     fft_row_fwd(L, L.tileA, V);
     V[32] = c_unit(conjf2(V[16]), e2);
@@ -752,10 +758,11 @@ __device__ __forceinline__ void lean_split(const Lane &L, f2 A, f2 Bv, int k, fl
 }
 
 // unit spectrum of one mic row, in place (paired layout)
+template <typename Hook = NoHook>
 __device__ __forceinline__ void lean_forward(const Lane &L, const uint32_t (&w)[16], f2 (&U)[33],
-                                             float e2)
+                                             float e2, Hook after_front = Hook())
 {
-    lean_spectrum(L, w, U, e2);
+    lean_spectrum(L, w, U, e2, after_front);
 #pragma unroll
     for (int k = 0; k < 16; k++)
         lean_split(L, U[k], U[31 - k], k, e2, U[k], U[31 - k]);
@@ -821,6 +828,27 @@ __device__ __forceinline__ int lane_res_sel(int l)
 }
 
 
+// max over each 32-lane half-wave, then both halves' results to every lane
+// (x: half-wave 0, y: half-wave 1) -- VALU/DPP only
+__device__ __forceinline__ f2 half_max2(float v)
+{
+    auto mx = [](float a, int b) { return fmaxf(a, __builtin_bit_cast(float, b)); };
+    int b = __builtin_bit_cast(int, v);
+    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, false));  // xor 1
+    b = __builtin_bit_cast(int, v);
+    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, false));  // xor 2
+    b = __builtin_bit_cast(int, v);
+    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x141, 0xF, 0xF, false));  // half-row mirror
+    b = __builtin_bit_cast(int, v);
+    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x140, 0xF, 0xF, false));  // row mirror
+    b = __builtin_bit_cast(int, v);
+    // row_bcast:15 into rows 1 and 3 (old = own value elsewhere)
+    v = mx(v, __builtin_amdgcn_update_dpp(b, b, 0x142, 0xA, 0xF, false));
+    const int r = __builtin_bit_cast(int, v);
+    return f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(r, 31)),
+              __builtin_bit_cast(float, __builtin_amdgcn_readlane(r, 63))};
+}
+
 // the lane id through an opaque move: lane-dependent values derived from it
 // are computed where they are used instead of being hoisted to the kernel's
 // start and held in registers across every phase
@@ -883,6 +911,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             stamp[nst++] = __builtin_amdgcn_s_memtime();          \
     } while (0)
     stamp[nst++] = __builtin_amdgcn_s_memtime();
+    stamp[14] = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
 #else
 #define LEAN_MARK() \
     do {            \
@@ -926,7 +955,6 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     {
         const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
         fetch(w0, f, 0);
-        fetch(w1, f, 1);
     }
 #else
     // table image: its loads first (L2 hits), then the first frames' words
@@ -940,18 +968,20 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         constexpr int SR = 4;  // image <= SR * NT * 16 B = 32 KiB (tdoa_phat1024_fits)
         uint4 img[SR];
 #pragma unroll
-        for (int r = 0; r < SR; r++)
-            if (tid + r * NT < n16)
-                img[r] = src[tid + r * NT];
+        for (int r = 0; r < SR; r++)  // unconditional (clamped) loads: straight-line
+            img[r] = src[tid + r * NT < n16 ? tid + r * NT : n16 - 1];  // code, counted waits
         const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
         fetch(w0, f, 0);
-        fetch(w1, f, 1);
 #pragma unroll
-        for (int r = 0; r < SR; r++)
-            if (tid + r * NT < n16)
-                dst[tid + r * NT] = img[r];
+        for (int r = 0; r < SR; r++)  // unconditional too (a clamped index rewrites
+            dst[tid + r * NT < n16 ? tid + r * NT : n16 - 1] = img[r];  // the last unit)
     }
     __syncthreads();
+    // keep the first row's use (and its wait) below the barrier: hoisted above
+    // it, every wave of the workgroup would wait for the latest wave's row
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+        asm volatile("" : "+v"(w0[t]));
 
 #endif
     const float invL = 1.0f / 2048.0f;
@@ -1005,7 +1035,10 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         };
 
         f2 U0[33], U1[33], y0, y31;
-        lean_forward(L, w0, U0, e2);
+        // the mics' rows are requested one at a time, each after the previous
+        // one's front end: at the kernel's start the memory system serves every
+        // wave's first row (8 MB) instead of all rows at once
+        lean_forward(L, w0, U0, e2, [&] { fetch(w1, f, 1); });
         LEAN_MARK();
         lean_forward(L, w1, U1, e2);
         LEAN_MARK();
@@ -1062,46 +1095,63 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
             wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
         wave_lds_order();  // the gathers read other lanes' score slots
+        LEAN_MARK();
         float gv[2] = {-INFINITY, -INFINITY};
         int gu[2] = {INT_MAX, INT_MAX};
         const char *ws = (const char *)wsc;
         // lane-strided: the 32 lanes of a gather read 32 consecutive tuples
         // (first-cell order: neighbouring cells, so equal or adjacent lag slots
-        // -- broadcasts and distinct banks instead of 4-way conflicts)
-        uint32_t q[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            q[i] = tups[64 * i + lane64];
-        for (int u0 = 0; u0 < Upad; u0 += 256) {
-            f2 Lg[4];
+        // -- broadcasts and distinct banks instead of 4-way conflicts).
+        // Software-pipelined by one step: the next step's tuple words and 12
+        // gathers are in flight while this step's sums and compares run (the
+        // loop is bound by LDS latency, not by its few VALU operations).
+        auto gather = [&](const uint32_t (&qq)[4], f2 (&g)[4][3]) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 // tuple fields are byte offsets of f2 slots in [p][KPAD]
-                const f2 l0 = lds_f2(ws, (int)(q[i] & 0x3FFu));
-                const f2 l1 = lds_f2(ws, P1K_KPAD * 8 + (int)((q[i] >> 10) & 0x3FFu));
-                const f2 l2 = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(q[i] >> 20));
-                Lg[i] = (l0 + l1) + l2;
+                g[i][0] = lds_f2(ws, (int)(qq[i] & 0x3FFu));
+                g[i][1] = lds_f2(ws, P1K_KPAD * 8 + (int)((qq[i] >> 10) & 0x3FFu));
+                g[i][2] = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(qq[i] >> 20));
             }
+        };
+        uint32_t q[4];
+        f2 g[4][3];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            q[i] = tups[64 * i + lane64];
+        gather(q, g);
+        for (int u0 = 0; u0 < Upad; u0 += 256) {
             const int un = u0 + 256 < Upad ? u0 + 256 : u0;
+            uint32_t qn[4];
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                q[i] = tups[un + 64 * i + lane64];
+                qn[i] = tups[un + 64 * i + lane64];
+            f2 gn[4][3];
+            gather(qn, gn);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
+                const f2 Lg = (g[i][0] + g[i][1]) + g[i][2];
                 const int u = u0 + 64 * i + lane64;  // ascending per lane
-                if (Lg[i].x > gv[0]) {
-                    gv[0] = Lg[i].x;
+                if (Lg.x > gv[0]) {
+                    gv[0] = Lg.x;
                     gu[0] = u;
                 }
-                if (Lg[i].y > gv[1]) {
-                    gv[1] = Lg[i].y;
+                if (Lg.y > gv[1]) {
+                    gv[1] = Lg.y;
                     gu[1] = u;
                 }
             }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    g[i][k] = gn[i][k];
         }
+        LEAN_MARK();
 #pragma unroll
         for (int j = 0; j < 2; j++)
             wave_argmax_to63(gv[j], gu[j]);
+        LEAN_MARK();
         if (lane64 == 63) {
             int cells[2];
 #pragma unroll
@@ -1126,6 +1176,8 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         LEAN_MARK();
     }
 #ifdef TDOA_DIAG
+    stamp[13] = __builtin_amdgcn_s_memtime();
+    stamp[15] = __builtin_amdgcn_s_memrealtime();
     if (lane64 == 0 && (blockIdx.x * NW + wave) < 4096)
         for (int i = 0; i < 16; i++)
             g_diag_p1k[(blockIdx.x * NW + wave) * 16 + i] = stamp[i];

@@ -36,7 +36,8 @@ buf = np.zeros(1 << 16, np.uint64)
 assert L.tdoa_diag_fetch_p1k(buf.ctypes.data_as(C.c_void_p), 1 << 16) == 0
 st = buf.reshape(-1, 16).astype(np.int64)
 st = st[st[:, 0] > 0]
-names = ["start", "staged", "mic0", "mic1", "pair01", "mic2+cross", "pair02", "pair12", "grid"]
+names = ["start", "staged", "mic0", "mic1", "pair01", "mic2+cross", "pair02", "pair12",
+         "grid-wsc", "grid-loop", "grid-argmax", "grid-out"]
 n = len(names)
 t = st[:, :n] - st[:, 0].min()
 print(f"B={B} waves={len(st)} kernel {e0.elapsed_time(e1) * 1e3:.1f} us (event, one launch)")
@@ -44,6 +45,12 @@ print("absolute (cycles from the first wave's start): p0 / p50 / p90 / max")
 for i, nm in enumerate(names):
     c = t[:, i]
     print(f"  {nm:11s} {c.min():8d} {np.median(c):8.0f} {np.percentile(c, 90):8.0f} {c.max():8d}")
+clk = (st[:, 13] - st[:, 0]) / ((st[:, 15] - st[:, 14]) / 100e6) / 1e9
+print(f"shader clock over a wave's life (s_memtime / s_memrealtime): p10 {np.percentile(clk, 10):.2f} "
+      f"p50 {np.median(clk):.2f} p90 {np.percentile(clk, 90):.2f} GHz")
+rt = st[:, 14] - st[:, 14].min()  # memrealtime is one chip-wide 100 MHz clock
+print(f"wave start (realtime, us): p50 {np.median(rt) / 100:.2f} max {rt.max() / 100:.2f}; "
+      f"wave end p50 {np.median(st[:, 15] - st[:, 14].min()) / 100:.2f} max {(st[:, 15] - st[:, 14].min()).max() / 100:.2f}")
 print("phase durations: p10 / p50 / p90")
 for i in range(1, n):
     d = t[:, i] - t[:, i - 1]
