@@ -55,3 +55,14 @@ print("phase durations: p10 / p50 / p90")
 for i in range(1, n):
     d = t[:, i] - t[:, i - 1]
     print(f"  {names[i]:11s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
+life = (st[:, 15] - st[:, 14]) / 100.0  # us
+end = (st[:, 15] - st[:, 14].min()) / 100.0
+blk = np.nonzero(buf.reshape(-1, 16)[:, 0] > 0)[0]  # global wave index = block * 8 + wave
+wv = blk % 8
+xcd = (blk // 8) % 8
+print("wave life (us): p10 %.2f p50 %.2f p90 %.2f p99 %.2f max %.2f" % tuple(np.percentile(life, [10, 50, 90, 99, 100])))
+print("wave end  (us): p10 %.2f p50 %.2f p90 %.2f p99 %.2f max %.2f" % tuple(np.percentile(end, [10, 50, 90, 99, 100])))
+print("end by wave-in-workgroup:", " ".join(f"{np.median(end[wv == w]):.1f}" for w in range(8)))
+print("end by block % 8 (XCD):  ", " ".join(f"{np.median(end[xcd == x]):.1f}" for x in range(8)))
+m0 = t[:, 2] - t[:, 1]
+print("mic0 phase by wave-in-workgroup (kcyc):", " ".join(f"{np.median(m0[wv == w]) / 1e3:.1f}" for w in range(8)))
