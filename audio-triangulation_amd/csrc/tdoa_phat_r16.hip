@@ -396,6 +396,331 @@ __global__ void __launch_bounds__(C / 16, 6) k_pair16(tdoa_kparams kp, tdoa_kout
         out.lags[fg * P + p] = bk - S;
 }
 
+// ------------------------------------------------------------ fused, per frame
+// k_frame16<C, MM>: one workgroup of 1024 threads per frame; the unit spectra
+// never leave the chip (the two-pass pair above writes them to a scratch and
+// reads them back, ~4x the frame's own bytes).  G = 16384 / C groups of
+// T = C / 16 threads (C = 4096: 4 groups, C = 2048: 8), M <= G = MM mics:
+//  1. forward: group g runs k_spec16's front end and three register passes on
+//     mic g in LDS slot g (padded C-point buffer); every thread then reads, for
+//     every mic, its bin-pair slots (b, C - b), b = tid + 1024 s (s < C / 2048),
+//     and keeps the split + PHAT-normalised U_m[b], U_m[C - b] in registers
+//     (thread 0 also U_m[C / 2], through LDS);
+//  2. pairs, G at a time: every thread writes the packed inverse input of its
+//     slots (k_pair16's pre-twiddle) for each pair of the round into that
+//     pair's buffer; group g then runs k_pair16's pruned inverse (pass 1 full,
+//     pass 2 outputs {0, 1, 14, 15}, pass 3 one output for 64 columns), the
+//     first argmax and the lag prior;
+//  3. gate from the frame's lags.
+// a thread index the compiler cannot prove loop-invariant: keeps twiddle
+// loads inside the pair-round loop instead of hoisted (and spilled) above it
+__device__ __forceinline__ int opaque_idx(int t)
+{
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+template <int C, int MM>
+__global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
+                                                     const int16_t *__restrict__ frames, float e2)
+{
+    constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = C + C / 16;
+    static_assert(MM == G, "one forward round: every mic has its own group");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f2 *bufs = (f2 *)smem;                    // [G][BUF]
+    f2 *xhalf = bufs + G * BUF;               // [MM] U_m[C / 2]
+    int *red = (int *)(xhalf + MM);           // [16] per-wave DC partial sums
+    int *lagl = red + 16;                     // [TDOA_MAX_PAIRS]
+    const int tid = threadIdx.x, g = tid / T, j = tid - g * T;
+    const int M = kp.M, P = kp.P, K = kp.K, S = kp.S;
+    const int64_t fr = blockIdx.x;
+    f2 *buf = bufs + g * BUF;
+    const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
+    const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+    const f2 *tt = reinterpret_cast<const f2 *>(kp.r16_tw);
+    const bool mic_on = g < M;
+
+    // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
+    {
+        const uint32_t *x = reinterpret_cast<const uint32_t *>(
+            frames + (fr * M + (mic_on ? g : 0)) * (int64_t)C);
+        uint32_t w[8], wn[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            w[s] = __builtin_nontemporal_load(x + j + T * s);
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            wn[s] = win[j + T * s];
+        int sum = 0;
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_r16, w[s]), v2s_r16{1, 1}, sum, false);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+            sum += __shfl_xor(sum, o, 64);
+        if ((tid & 63) == 0)
+            red[tid >> 6] = sum;
+        __syncthreads();
+        sum = 0;
+#pragma unroll
+        for (int wv = 0; wv < T / 64; wv++)
+            sum += red[g * (T / 64) + wv];
+        const uint32_t off = (uint32_t)(sum >> kp.log2N) & 0xFFu;
+        const uint32_t off2 = off | (off << 16);
+        f2 v[16];
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const uint32_t d = (w[s] | 0x01000100u) - off2;
+            const float s0 = (float)(int8_t)(d & 0xFFu), s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+            const float w0 = (float)(int16_t)(wn[s] & 0xFFFFu) * (1.0f / 128.0f);
+            const float w1 = (float)(int16_t)(wn[s] >> 16) * (1.0f / 128.0f);
+            v[s] = f2{floorf(s0 * w0), floorf(s1 * w1)};
+        }
+        if constexpr (R1 == 16) {
+#pragma unroll
+            for (int s = 8; s < 16; s++)
+                v[s] = f2{0.0f, 0.0f};
+            dftp<16, false, true>(v);
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                sts2(buf, 16 * j + r, v[brev<16>(r)]);
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                f2 u[8];
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    u[r] = v[2 * r + h];
+#pragma unroll
+                for (int r = 4; r < 8; r++)
+                    u[r] = f2{0.0f, 0.0f};
+                dftp<8, false, true>(u);
+                const int jv = j + 128 * h;
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+                    sts2(buf, 8 * jv + r, u[brev<8>(r)]);
+            }
+        }
+        __syncthreads();
+        {
+            const int k = j % R1;
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                v[r] = lds2(buf, j + T * r);
+#pragma unroll
+            for (int r = 1; r < 16; r++)
+                v[r] = c_mul(v[r], tw16h(tt, r, k));
+            dftp<16, false, false>(v);
+            __syncthreads();
+            const int o = (j / R1) * 16 * R1 + k;
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                sts2(buf, o + R1 * r, v[brev<16>(r)]);
+        }
+        __syncthreads();
+        {
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                v[r] = lds2(buf, j + T * r);
+#pragma unroll
+            for (int r = 1; r < 16; r++)
+                v[r] = c_mul(v[r], twC(tt, r, j));
+            dftp<16, false, false>(v);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
+                sts2(buf, j + T * q, v[brev<16>(q)]);
+        }
+        __syncthreads();
+    }
+    // split + unit normalisation of every mic at this thread's bin pairs:
+    // X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), X[C-b] = conj(e + i W od)
+    // (b = 0: its partner output is X[C])
+    f2 Ub[MM][NS], Un[MM][NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int b = tid + 1024 * s;
+        const f2 wb = tw2[b];
+#pragma unroll
+        for (int m = 0; m < MM; m++) {
+            if (m < M) {
+                const f2 *zb = bufs + m * BUF;
+                const f2 z = lds2(zb, b), zp = lds2(zb, (C - b) & (C - 1));
+                const f2 e = c_addconj(z, zp);
+                const f2 od = c_mul(c_subconj(z, zp), wb);
+                Ub[m][s] = c_unit(c_add_mi(e, od), e2);
+                Un[m][s] = c_unit(c_conj_add_i(e, od), e2);
+            } else {
+                Ub[m][s] = Un[m][s] = f2{0.0f, 0.0f};
+            }
+        }
+    }
+    if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
+        const f2 zh = lds2(bufs + tid * BUF, C / 2);
+        xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
+    }
+    __syncthreads();  // slots consumed: they become the pairs' buffers
+
+    // ---- 2. pairs, G per round
+    const float invL = 1.0f / (float)(2 * C);
+    for (int p0 = 0; p0 < P; p0 += G) {
+        const int tl = opaque_idx(tid), jl = tl - g * T;
+        // packed inverse input Y of pair p0 + gg into buffer gg (all threads)
+#pragma unroll
+        for (int gg = 0; gg < G; gg++) {
+            const int p = p0 + gg;
+            if (p >= P)
+                break;
+            const int pi = kp.pair_i[p], pj = kp.pair_j[p];
+            f2 *yb = bufs + gg * BUF;
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                const int b = tl + 1024 * s;
+                f2 Ri = f2{0, 0}, Rn = f2{0, 0};
+#pragma unroll
+                for (int m = 0; m < MM; m++) {  // register arrays: select by unrolled index
+                    if (m == pi) {
+                        Ri = Ub[m][s];
+                        Rn = Un[m][s];
+                    }
+                }
+                f2 Rj = f2{0, 0}, Rjn = f2{0, 0};
+#pragma unroll
+                for (int m = 0; m < MM; m++) {
+                    if (m == pj) {
+                        Rj = Ub[m][s];
+                        Rjn = Un[m][s];
+                    }
+                }
+                const f2 Rk = c_conjmul(Ri, Rj), Rq = c_conjmul(Rn, Rjn);  // R[b], R[C-b]
+                const f2 ss = c_addconj(Rk, Rq);
+                const f2 qq = c_mulconj(c_subconj(Rk, Rq), tw2[b]);
+                sts2(yb, b, c_add_i(ss, qq));
+                if (b != 0)
+                    sts2(yb, C - b, c_conj_add_mi(ss, qq));
+            }
+            if (tl == 0) {  // Y[C/2] from R[C/2] alone
+                const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
+                sts2(yb, C / 2, c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), tw2[C / 2])));
+            }
+        }
+        __syncthreads();
+        const int p = p0 + g;
+        const bool pair_on = p < P;
+        // inverse pass 1 (radix 16, Ns = 1)
+        f2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = lds2(buf, jl + T * r);
+        dftp<16, true, false>(v);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            sts2(buf, 16 * jl + r, v[brev<16>(r)]);
+        __syncthreads();
+        // pass 2: outputs r'' in {0, 1, 14, 15} only
+        const int k = jl & 15;
+        f2 x0 = f2{0, 0}, x1 = f2{0, 0}, x14 = f2{0, 0}, x15 = f2{0, 0};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
+            f2 l0 = lds2(buf, jl + T * r), l1 = lds2(buf, jl + T * (r + 4));
+            const f2 h0 = c_mulconj(lds2(buf, jl + T * (r + 8)), tw256(tt, r + 8, k));
+            const f2 h1 = c_mulconj(lds2(buf, jl + T * (r + 12)), tw256(tt, r + 12, k));
+            if (r)
+                l0 = c_mulconj(l0, tw256(tt, r, k));
+            l1 = c_mulconj(l1, tw256(tt, r + 4, k));
+            const f2 a0 = l0 + h0, a1 = l1 + h1;
+            const f2 d0 = dif_tw<true>(l0, h0, 2 * r), d1 = dif_tw<true>(l1, h1, 2 * (r + 4));
+            x0 = x0 + (a0 + a1);
+            x1 = x1 + (d0 + d1);
+            x14 = x14 + (r ? dif_tw<false>(a0, a1, 4 * r) : a0 - a1);
+            x15 = x15 + (r ? dif_tw<false>(d0, d1, 4 * r) : d0 - d1);
+        }
+        __syncthreads();
+        {
+            const int o = (jl >> 4) * 64 + k;
+            sts2(buf, o, x0);
+            sts2(buf, o + 16, x1);
+            sts2(buf, o + 32, x14);
+            sts2(buf, o + 48, x15);
+        }
+        __syncthreads();
+        // pass 3 by the group's first wave: one output per column
+        if (jl < 64 && pair_on) {
+            const int l = jl;
+            const int jc = l < 32 ? l : 192 + l;
+            const int mm = 64 - l;
+            f2 y = lds2(buf, l);
+#pragma unroll
+            for (int r = 1; r < R1; r++) {
+                const f2 u = lds2(buf, 64 * r + l);
+                y = y + (l < 32 ? c_mulconj(u, twC(tt, r, jc)) : c_mul(u, twC(tt, r, mm)));
+            }
+            const int n = l < 32 ? l : -mm;
+            const int ka = 2 * n + S, kb = 2 * n + 1 + S;
+            const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
+            const float sa = y.x * invL, sb = y.y * invL;
+            float bv = -INFINITY;
+            int bk = INT_MAX;
+            if (oka) {
+                bv = sa;
+                bk = ka;
+            }
+            if (okb && (sb > bv || bk == INT_MAX)) {
+                bv = sb;
+                bk = kb;
+            }
+            wave_argmax_to63(bv, bk);  // first maximum: the lowest lag wins ties
+            bk = __builtin_amdgcn_readlane(bk, 63);
+            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
+            const size_t gb = (size_t)(fr * P + p) * K;
+            if (oka) {
+                const int dd = ka > bk ? ka - bk : bk - ka;
+                if (out.scores_f)
+                    out.scores_f[gb + ka] = sa;
+                if (out.weighted_f)
+                    out.weighted_f[gb + ka] = sa * kp.prior[dd];
+            }
+            if (okb) {
+                const int dd = kb > bk ? kb - bk : bk - kb;
+                if (out.scores_f)
+                    out.scores_f[gb + kb] = sb;
+                if (out.weighted_f)
+                    out.weighted_f[gb + kb] = sb * kp.prior[dd];
+            }
+            if (l == 0) {
+                out.lags[fr * P + p] = bk - S;
+                lagl[p] = bk - S;
+            }
+        }
+        __syncthreads();  // the buffers are rewritten by the next round
+    }
+    if (tid == 0 && out.gate) {
+        int tot = 0;
+        for (int q = 0; q < P; q++)
+            tot += lagl[q] * lagl[q];
+        out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+    }
+}
+
+template <int C, int MM>
+int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+                   float e2, hipStream_t st)
+{
+    constexpr int G = 16384 / C, BUF = C + C / 16;
+    const size_t lds = (size_t)G * BUF * sizeof(f2) + MM * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4;
+    if (B > INT_MAX)
+        return tdoa_set_error(-1, "GCC_PHAT: batch too large for one launch");
+    hipLaunchKernelGGL((k_frame16<C, MM>), dim3((unsigned)B), dim3(1024), lds, st, kp, out, frames, e2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "k_frame16 launch: %s", hipGetErrorString(e));
+        return tdoa_set_error(-2, msg);
+    }
+    return 0;
+}
+
 __global__ void k_r16_gate(const int32_t *__restrict__ lags, uint8_t *__restrict__ gate, int64_t B, int P)
 {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -462,6 +787,18 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (!(e2 >= 1e-30f))
         e2 = 1e-30f;
     hipStream_t st = (hipStream_t)stream;
+    // TDOA_PHAT_FUSED=1: the per-frame fused kernel (spectra on chip; M <= 4 at
+    // frame_len 4096, M <= 8 at 2048).  Off by default: its whole-workgroup
+    // barriers (one 1024-thread workgroup per CU) measured slower than the
+    // two-pass kernels (config 3: 8.80 vs 7.86 ms, config 4: 254 vs 198 ms)
+    static const int use_fused = [] {
+        const char *s = getenv("TDOA_PHAT_FUSED");
+        return s ? atoi(s) : 0;
+    }();
+    if (use_fused && kp.N == 4096 && kp.M <= 4)
+        return launch_frame16<4096, 4>(kp, out, frames, B, e2, st);
+    if (use_fused && kp.N == 2048 && kp.M <= 8)
+        return launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
     return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)
                         : launch_r16<2048>(kp, out, frames, B, e2, scratch, scratch_bytes, st);
 }
