@@ -917,6 +917,28 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     do {            \
     } while (0)
 #endif
+    // issue balance between the two waves of a SIMD (waves w and w ^ 4: a
+    // workgroup's waves are dealt to the CU's four SIMDs in turn).  The SIMD
+    // issues oldest-first, so without this wave w runs ahead and wave w ^ 4
+    // finishes its last ~9 us alone, with nothing to hide its latencies; here
+    // a wave that has passed more phase boundaries than its partner drops to
+    // the low priority until the partner catches up
+    __shared__ int prog[NW];
+    if (lane64 == 0)
+        prog[wave] = 0;
+    __builtin_amdgcn_s_setprio(2);
+    int phase = 0;
+    auto balance = [&]() {
+        volatile int *pv = prog;
+        ++phase;
+        if (lane64 == 0)
+            pv[wave] = phase;
+        const int other = __builtin_amdgcn_readfirstlane(pv[wave ^ 4]);
+        if (phase > other)
+            __builtin_amdgcn_s_setprio(0);
+        else
+            __builtin_amdgcn_s_setprio(2);
+    };
     Lane L;
     L.hw = hw;
     L.lane = tid & 31;
@@ -1038,10 +1060,15 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         // the mics' rows are requested one at a time, each after the previous
         // one's front end: at the kernel's start the memory system serves every
         // wave's first row (8 MB) instead of all rows at once
-        lean_forward(L, w0, U0, e2, [&] { fetch(w1, f, 1); });
+        lean_forward(L, w0, U0, e2, [&] {
+            fetch(w1, f, 1);
+            balance();
+        });
         LEAN_MARK();
-        lean_forward(L, w1, U1, e2);
+        balance();
+        lean_forward(L, w1, U1, e2, [&] { balance(); });
         LEAN_MARK();
+        balance();
         {
             f2 v[32];
             lean_pretwiddle<true>(L, U0, U1, v);  // pair 0: (0, 1)
@@ -1053,8 +1080,10 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         }
         finish_pair(0, y0, y31);
         LEAN_MARK();
+        balance();
         lean_forward_cross(L, w2, U0, U1, e2);  // pairs 1: (0, 2), 2: (1, 2)
         LEAN_MARK();
+        balance();
         {
             f2 v[32];
             lean_pretwiddle<false>(L, U0, U0, v);
@@ -1063,6 +1092,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         }
         finish_pair(1, y0, y31);
         LEAN_MARK();
+        balance();
         {
             f2 v[32];
             lean_pretwiddle<false>(L, U1, U1, v);
@@ -1071,6 +1101,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         }
         finish_pair(2, y0, y31);
         LEAN_MARK();
+        balance();
         if (live && L.lane == 0 && out.gate)
             out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
 
@@ -1294,7 +1325,7 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp)
     // grid scores of a wave's four frames live in its tiles: [3][KPAD] float4 = 6 KiB
     static_assert(3 * P1K_KPAD * 16 <= p1k_wave_lds<false>(), "grid scores exceed the wave's tiles");
     if (g_p1k_waves == 8)
-        return p1k_lds<8, false>(kp.U) <= 160 * 1024;
+        return p1k_lds<8, false>(kp.U) + 64 <= 160 * 1024;  // + the static progress words
     return p1k_lds<4, true>(kp.U) <= 160 * 1024;
 }
 
