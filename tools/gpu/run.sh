@@ -12,6 +12,8 @@
 #   kstats[:CFG[:ENGINE]] rocprofv3 --kernel-trace --stats of the bench
 #   pmc[:CFG[:ENGINE]]    FETCH_SIZE and WRITE_SIZE passes (one run each)
 #   sq[:CFG[:ENGINE]]     two SQ counter passes (waves, VALU, LDS, waits)
+#   pmcx:CFG:ENGINE:NAME:C1,C2,..  one pass of the listed counters (mind the
+#                         per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
 #   smoke                 __graft_entry__.smoke()
 #
 # Env: TAG (output subdirectory, default "cur"), STEPS (bench steps),
@@ -85,6 +87,14 @@ for step in "$@"; do
         prof "sq2_c${c}_$e" --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU \
             SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA || exit 27
         echo "sq c$c $e done"
+        ;;
+    pmcx)
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat); n=$(field "$step" 4 x)
+        ctr=$(field "$step" 5 "")
+        [ -z "$ctr" ] && { echo "pmcx needs counters"; exit 2; }
+        PARGS="--config $c --engine $e --steps 24 --warmup 2 --no-cpu $BENCH_ARGS"
+        prof "${n}_c${c}_$e" --pmc ${ctr//,/ } || exit 29
+        echo "pmcx $n c$c $e done"
         ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
