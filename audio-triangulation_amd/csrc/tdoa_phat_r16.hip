@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <climits>
+#include <type_traits>
 #include <cstdio>
 
 #include "tdoa_cplx.h"
@@ -397,10 +398,14 @@ __global__ void __launch_bounds__(C / 16, 6) k_pair16(tdoa_kparams kp, tdoa_kout
 }
 
 // ------------------------------------------------------------ fused, per frame
-// k_frame16<C, MM>: one workgroup of 1024 threads per frame; the unit spectra
+// k_frame16<C, M>: one workgroup of 1024 threads per frame; the unit spectra
 // never leave the chip (the two-pass pair above writes them to a scratch and
 // reads them back, ~4x the frame's own bytes).  G = 16384 / C groups of
-// T = C / 16 threads (C = 4096: 4 groups, C = 2048: 8), M <= G = MM mics:
+// T = C / 16 threads (C = 4096: 4 groups, C = 2048: 8), M <= G mics.  The
+// pairs are the host's lexicographic (i, j) order resolved at compile time (a
+// runtime pair index selected each spectrum through M-way v_cndmask chains,
+// which cost more than the transforms), and the twiddle tables are staged in
+// LDS (each pass reads them right after a barrier):
 //  1. forward: group g runs k_spec16's front end and three register passes on
 //     mic g in LDS slot g (padded C-point buffer); every thread then reads, for
 //     every mic, its bin-pair slots (b, C - b), b = tid + 1024 s (s < C / 2048),
@@ -420,25 +425,83 @@ __device__ __forceinline__ int opaque_idx(int t)
     return t;
 }
 
-template <int C, int MM>
+// pairs in the host's lexicographic order (tdoa_capi.cpp): pair p = (i, j)
+template <int M>
+__host__ __device__ constexpr int pair_first(int p)
+{
+    int i = 0;
+    while (p >= M - 1 - i) {
+        p -= M - 1 - i;
+        i++;
+    }
+    return i;
+}
+template <int M>
+__host__ __device__ constexpr int pair_second(int p)
+{
+    int i = 0;
+    while (p >= M - 1 - i) {
+        p -= M - 1 - i;
+        i++;
+    }
+    return i + 1 + p;
+}
+static_assert(pair_first<4>(5) == 2 && pair_second<4>(5) == 3 && pair_second<8>(6) == 7, "pair order");
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+#ifdef TDOA_DIAG
+// diagnostic build only: s_memtime per phase boundary, per wave of the first 256 frames
+__device__ unsigned long long g_diag_f16[1 << 16];
+#define F16_MARK()                                       \
+    do {                                                 \
+        if (nst < 14)                                    \
+            stamp[nst++] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define F16_MARK() \
+    do {           \
+    } while (0)
+#endif
+
+template <int C, int M>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, float e2)
 {
     constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = C + C / 16;
-    static_assert(MM == G, "one forward round: every mic has its own group");
+    static_assert(M >= 2 && M <= G, "one forward round: every mic has its own group");
+    constexpr int P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *bufs = (f2 *)smem;                    // [G][BUF]
-    f2 *xhalf = bufs + G * BUF;               // [MM] U_m[C / 2]
-    int *red = (int *)(xhalf + MM);           // [16] per-wave DC partial sums
+    f2 *xhalf = bufs + G * BUF;               // [G] U_m[C / 2]
+    int *red = (int *)(xhalf + G);            // [16] per-wave DC partial sums
     int *lagl = red + 16;                     // [TDOA_MAX_PAIRS]
+    f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
     const int tid = threadIdx.x, g = tid / T, j = tid - g * T;
-    const int M = kp.M, P = kp.P, K = kp.K, S = kp.S;
+    const int K = kp.K, S = kp.S;
     const int64_t fr = blockIdx.x;
     f2 *buf = bufs + g * BUF;
     const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
     const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
-    const f2 *tt = reinterpret_cast<const f2 *>(kp.r16_tw);
+    // the twiddle tables in LDS (6 KiB): every pass reads them right after a
+    // barrier, where a global (L2) round trip would stall the whole workgroup
+    if (threadIdx.x < 3 * 16 * 16)  // 8-B units: kp.r16_tw is 8-B aligned
+        ttl[threadIdx.x] = reinterpret_cast<const f2 *>(kp.r16_tw)[threadIdx.x];
+    const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const bool mic_on = g < M;
+#ifdef TDOA_DIAG
+    unsigned long long stamp[16] = {};
+    int nst = 0;
+    stamp[14] = __builtin_amdgcn_s_memrealtime();
+#endif
+    F16_MARK();
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
     {
@@ -533,78 +596,69 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
         __syncthreads();
     }
+    F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
     // X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), X[C-b] = conj(e + i W od)
     // (b = 0: its partner output is X[C])
-    f2 Ub[MM][NS], Un[MM][NS];
+    f2 Ub[M][NS], Un[M][NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const int b = tid + 1024 * s;
         const f2 wb = tw2[b];
 #pragma unroll
-        for (int m = 0; m < MM; m++) {
-            if (m < M) {
-                const f2 *zb = bufs + m * BUF;
-                const f2 z = lds2(zb, b), zp = lds2(zb, (C - b) & (C - 1));
-                const f2 e = c_addconj(z, zp);
-                const f2 od = c_mul(c_subconj(z, zp), wb);
-                Ub[m][s] = c_unit(c_add_mi(e, od), e2);
-                Un[m][s] = c_unit(c_conj_add_i(e, od), e2);
-            } else {
-                Ub[m][s] = Un[m][s] = f2{0.0f, 0.0f};
-            }
+        for (int m = 0; m < M; m++) {
+            const f2 *zb = bufs + m * BUF;
+            const f2 z = lds2(zb, b), zp = lds2(zb, (C - b) & (C - 1));
+            const f2 e = c_addconj(z, zp);
+            const f2 od = c_mul(c_subconj(z, zp), wb);
+            Ub[m][s] = c_unit(c_add_mi(e, od), e2);
+            Un[m][s] = c_unit(c_conj_add_i(e, od), e2);
         }
     }
+    f2 twb[NS];  // W_2C^b of this thread's bins, for every pair's pre-twiddle
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+        twb[s] = tw2[tid + 1024 * s];
+    const f2 twh = tw2[C / 2];
     if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
         const f2 zh = lds2(bufs + tid * BUF, C / 2);
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
     }
     __syncthreads();  // slots consumed: they become the pairs' buffers
+    F16_MARK();  // unit spectra in registers
 
-    // ---- 2. pairs, G per round
+    // ---- 2. pairs, G per round (rounds and pair slots unrolled: every
+    // register index below is a compile-time constant)
     const float invL = 1.0f / (float)(2 * C);
-    for (int p0 = 0; p0 < P; p0 += G) {
+    static_for<0, ROUNDS>([&](auto rc) {
+        constexpr int p0 = decltype(rc)::value * G;
         const int tl = opaque_idx(tid), jl = tl - g * T;
         // packed inverse input Y of pair p0 + gg into buffer gg (all threads)
+        static_for<0, G>([&](auto gc) {
+            constexpr int pc = p0 + decltype(gc)::value;
+            if constexpr (pc < P) {
+                constexpr int pi = pair_first<M>(pc), pj = pair_second<M>(pc);
+                f2 *yb = bufs + decltype(gc)::value * BUF;
 #pragma unroll
-        for (int gg = 0; gg < G; gg++) {
-            const int p = p0 + gg;
-            if (p >= P)
-                break;
-            const int pi = kp.pair_i[p], pj = kp.pair_j[p];
-            f2 *yb = bufs + gg * BUF;
-#pragma unroll
-            for (int s = 0; s < NS; s++) {
-                const int b = tl + 1024 * s;
-                f2 Ri = f2{0, 0}, Rn = f2{0, 0};
-#pragma unroll
-                for (int m = 0; m < MM; m++) {  // register arrays: select by unrolled index
-                    if (m == pi) {
-                        Ri = Ub[m][s];
-                        Rn = Un[m][s];
-                    }
+                for (int s = 0; s < NS; s++) {
+                    const int b = tl + 1024 * s;
+                    const f2 Rk = c_conjmul(Ub[pi][s], Ub[pj][s]);  // R[b]
+                    const f2 Rq = c_conjmul(Un[pi][s], Un[pj][s]);  // R[C-b]
+                    const f2 ss = c_addconj(Rk, Rq);
+                    const f2 qq = c_mulconj(c_subconj(Rk, Rq), twb[s]);
+                    sts2(yb, b, c_add_i(ss, qq));
+                    if (b != 0)
+                        sts2(yb, C - b, c_conj_add_mi(ss, qq));
                 }
-                f2 Rj = f2{0, 0}, Rjn = f2{0, 0};
-#pragma unroll
-                for (int m = 0; m < MM; m++) {
-                    if (m == pj) {
-                        Rj = Ub[m][s];
-                        Rjn = Un[m][s];
-                    }
+                if (tl == 0) {  // Y[C/2] from R[C/2] alone
+                    const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
+                    sts2(yb, C / 2,
+                         c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), twh)));
                 }
-                const f2 Rk = c_conjmul(Ri, Rj), Rq = c_conjmul(Rn, Rjn);  // R[b], R[C-b]
-                const f2 ss = c_addconj(Rk, Rq);
-                const f2 qq = c_mulconj(c_subconj(Rk, Rq), tw2[b]);
-                sts2(yb, b, c_add_i(ss, qq));
-                if (b != 0)
-                    sts2(yb, C - b, c_conj_add_mi(ss, qq));
             }
-            if (tl == 0) {  // Y[C/2] from R[C/2] alone
-                const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
-                sts2(yb, C / 2, c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), tw2[C / 2])));
-            }
-        }
+        });
         __syncthreads();
+        F16_MARK();  // the round's Y buffers written
         const int p = p0 + g;
         const bool pair_on = p < P;
         // inverse pass 1 (radix 16, Ns = 1)
@@ -694,24 +748,34 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
-    }
+        F16_MARK();
+    });
     if (tid == 0 && out.gate) {
         int tot = 0;
         for (int q = 0; q < P; q++)
             tot += lagl[q] * lagl[q];
         out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
     }
+#ifdef TDOA_DIAG
+    stamp[15] = __builtin_amdgcn_s_memrealtime();
+    stamp[13] = __builtin_amdgcn_s_memtime();
+    if ((tid & 63) == 0 && blockIdx.x < 256)
+        for (int i = 0; i < 16; i++)
+            g_diag_f16[(blockIdx.x * 16 + (tid >> 6)) * 16 + i] = stamp[i];
+#endif
 }
+#undef F16_MARK
 
-template <int C, int MM>
+template <int C, int M>
 int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                    float e2, hipStream_t st)
 {
     constexpr int G = 16384 / C, BUF = C + C / 16;
-    const size_t lds = (size_t)G * BUF * sizeof(f2) + MM * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4;
+    const size_t lds = (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
+                       3 * 16 * 16 * sizeof(f2);
     if (B > INT_MAX)
         return tdoa_set_error(-1, "GCC_PHAT: batch too large for one launch");
-    hipLaunchKernelGGL((k_frame16<C, MM>), dim3((unsigned)B), dim3(1024), lds, st, kp, out, frames, e2);
+    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)B), dim3(1024), lds, st, kp, out, frames, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];
@@ -787,18 +851,33 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (!(e2 >= 1e-30f))
         e2 = 1e-30f;
     hipStream_t st = (hipStream_t)stream;
-    // TDOA_PHAT_FUSED=1: the per-frame fused kernel (spectra on chip; M <= 4 at
-    // frame_len 4096, M <= 8 at 2048).  Off by default: its whole-workgroup
-    // barriers (one 1024-thread workgroup per CU) measured slower than the
-    // two-pass kernels (config 3: 8.80 vs 7.86 ms, config 4: 254 vs 198 ms)
+    // the per-frame fused kernel (spectra on chip) for M = 3, 4 at frame_len 4096
+    // and M = 4, 8 at 2048 (config 3: 6.41 vs 7.86 ms per 65536 frames, config
+    // 4: 161 vs 198 ms per 1e6); TDOA_PHAT_FUSED=0 keeps the two-pass kernels
     static const int use_fused = [] {
         const char *s = getenv("TDOA_PHAT_FUSED");
-        return s ? atoi(s) : 0;
+        return s ? atoi(s) : 1;
     }();
-    if (use_fused && kp.N == 4096 && kp.M <= 4)
+    if (use_fused && kp.N == 4096 && kp.M == 4)
         return launch_frame16<4096, 4>(kp, out, frames, B, e2, st);
-    if (use_fused && kp.N == 2048 && kp.M <= 8)
+    if (use_fused && kp.N == 4096 && kp.M == 3)
+        return launch_frame16<4096, 3>(kp, out, frames, B, e2, st);
+    if (use_fused && kp.N == 2048 && kp.M == 8)
         return launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
+    if (use_fused && kp.N == 2048 && kp.M == 4)
+        return launch_frame16<2048, 4>(kp, out, frames, B, e2, st);
     return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)
                         : launch_r16<2048>(kp, out, frames, B, e2, scratch, scratch_bytes, st);
 }
+
+#ifdef TDOA_DIAG
+extern "C" int tdoa_diag_fetch_f16(unsigned long long *host, int n)
+{
+    if (n > (1 << 16))
+        n = 1 << 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_f16), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif
