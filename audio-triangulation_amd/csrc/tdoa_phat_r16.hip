@@ -473,7 +473,8 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 
 template <int C, int M>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
-                                                     const int16_t *__restrict__ frames, float e2)
+                                                     const int16_t *__restrict__ frames, int64_t B,
+                                                     float e2)
 {
     constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = C + C / 16;
     static_assert(M >= 2 && M <= G, "one forward round: every mic has its own group");
@@ -484,9 +485,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     int *red = (int *)(xhalf + G);            // [16] per-wave DC partial sums
     int *lagl = red + 16;                     // [TDOA_MAX_PAIRS]
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
-    const int tid = threadIdx.x, g = tid / T, j = tid - g * T;
+    const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
-    const int64_t fr = blockIdx.x;
     f2 *buf = bufs + g * BUF;
     const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
     const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
@@ -495,22 +495,34 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     if (threadIdx.x < 3 * 16 * 16)  // 8-B units: kp.r16_tw is 8-B aligned
         ttl[threadIdx.x] = reinterpret_cast<const f2 *>(kp.r16_tw)[threadIdx.x];
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
-    const bool mic_on = g < M;
+    const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
 #ifdef TDOA_DIAG
     unsigned long long stamp[16] = {};
     int nst = 0;
     stamp[14] = __builtin_amdgcn_s_memrealtime();
 #endif
-    F16_MARK();
+    // persistent over frames (one workgroup per CU): the next frame's words are
+    // requested when the pair rounds start, so their HBM latency hides behind
+    // them instead of opening every frame
+    uint32_t w[8];
+    auto fetch = [&](int64_t f) {
+        const uint32_t *x = reinterpret_cast<const uint32_t *>(frames + (f * M + mg) * (int64_t)C) +
+                            ((int)threadIdx.x - g * T);
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            w[s] = __builtin_nontemporal_load(x + T * s);
+    };
+    fetch(blockIdx.x);
+    for (int64_t fr = blockIdx.x; fr < B; fr += gridDim.x) {
+    // thread indices the compiler cannot prove loop-invariant: the passes'
+    // twiddle reads stay in the body instead of being hoisted (and spilled)
+    const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T;
+    if (fr == blockIdx.x)
+        F16_MARK();
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
     {
-        const uint32_t *x = reinterpret_cast<const uint32_t *>(
-            frames + (fr * M + (mic_on ? g : 0)) * (int64_t)C);
-        uint32_t w[8], wn[8];
-#pragma unroll
-        for (int s = 0; s < 8; s++)
-            w[s] = __builtin_nontemporal_load(x + j + T * s);
+        uint32_t wn[8];
 #pragma unroll
         for (int s = 0; s < 8; s++)
             wn[s] = win[j + T * s];
@@ -596,7 +608,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
         __syncthreads();
     }
-    F16_MARK();  // forward transforms done
+    if (fr == blockIdx.x)
+        F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
     // X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), X[C-b] = conj(e + i W od)
     // (b = 0: its partner output is X[C])
@@ -625,7 +638,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
     }
     __syncthreads();  // slots consumed: they become the pairs' buffers
-    F16_MARK();  // unit spectra in registers
+    if (fr == blockIdx.x)
+        F16_MARK();  // unit spectra in registers
+    {
+        const int64_t fn = fr + gridDim.x;
+        fetch(fn < B ? fn : fr);  // the next frame's words (or a harmless re-read)
+    }
 
     // ---- 2. pairs, G per round (rounds and pair slots unrolled: every
     // register index below is a compile-time constant)
@@ -658,7 +676,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             }
         });
         __syncthreads();
-        F16_MARK();  // the round's Y buffers written
+        if (fr == blockIdx.x)
+            F16_MARK();  // the round's Y buffers written
         const int p = p0 + g;
         const bool pair_on = p < P;
         // inverse pass 1 (radix 16, Ns = 1)
@@ -748,7 +767,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
-        F16_MARK();
+        if (fr == blockIdx.x)
+            F16_MARK();
     });
     if (tid == 0 && out.gate) {
         int tot = 0;
@@ -757,11 +777,16 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
     }
 #ifdef TDOA_DIAG
-    stamp[15] = __builtin_amdgcn_s_memrealtime();
-    stamp[13] = __builtin_amdgcn_s_memtime();
-    if ((tid & 63) == 0 && blockIdx.x < 256)
+    if (fr == blockIdx.x) {
+        stamp[15] = __builtin_amdgcn_s_memrealtime();
+        stamp[13] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    }  // frames
+#ifdef TDOA_DIAG
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)
         for (int i = 0; i < 16; i++)
-            g_diag_f16[(blockIdx.x * 16 + (tid >> 6)) * 16 + i] = stamp[i];
+            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + i] = stamp[i];
 #endif
 }
 #undef F16_MARK
@@ -773,9 +798,14 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
     constexpr int G = 16384 / C, BUF = C + C / 16;
     const size_t lds = (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
                        3 * 16 * 16 * sizeof(f2);
-    if (B > INT_MAX)
-        return tdoa_set_error(-1, "GCC_PHAT: batch too large for one launch");
-    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)B), dim3(1024), lds, st, kp, out, frames, e2);
+    if (B <= 0)
+        return 0;
+    const int res = tdoa_resident_blocks((const void *)k_frame16<C, M>, 1024, lds);
+    if (res < 1)
+        return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
+    const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
+    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B,
+                       e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];
