@@ -26,7 +26,8 @@ def per_kernel(path, counter):
         return {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            name = (r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+                    .split("(")[0])
             vals[name].append(float(r["Counter_Value"]))
     return {k: v[len(v) // 4:] for k, v in vals.items() if v[len(v) // 4:]}
 
