@@ -216,6 +216,9 @@ struct tdoa_ctx {
     size_t rscratch_bytes = 0;
     void *d_cscratch = nullptr;
     size_t cscratch_bytes = 0;
+    std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx
+    void *d_bb = nullptr;
+    int bb_NT = 0;
     float *d_mic = nullptr;  // [M][2]
     uint8_t *d_lut = nullptr;  // [P][G]
     // GCC_PHAT spectrum scratch for the two-pass shapes (M > 3 or N > 2048):
@@ -246,6 +249,8 @@ void reference_triangle(float *xy)
 }
 
 inline float hypot3(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
+void build_bb_tiles(tdoa_ctx *c);
 
 // vga_heatmap.h:48-93, generalised to lexicographic pairs of M mics.
 void build_lut(tdoa_ctx *c)
@@ -300,6 +305,62 @@ void build_lut(tdoa_ctx *c)
         }
     }
     c->U = (int)c->tuple_cell.size();
+    build_bb_tiles(c);
+}
+
+// Tables of the exact branch-and-bound grid solve (k_grid_bb, tdoa_grid.hip):
+// the distinct tuples regrouped by the TILE x TILE block of grid cells their
+// first cell lies in (entries of at most 64 tuples, one per lane), and for
+// every entry and pair the range of lag indices its tuples use.  The bound of
+// an entry is the sum over pairs of the weighted-score maximum over that range.
+void build_bb_tiles(tdoa_ctx *c)
+{
+    constexpr int TILE = 8, CAP = 64;
+    const int P = c->P, TW = c->TW, U = c->U;
+    const int tx = (c->W + TILE - 1) / TILE, ty = (c->H + TILE - 1) / TILE;
+    std::vector<std::vector<int>> members((size_t)tx * ty);
+    for (int u = 0; u < U; u++) {
+        const int cell = c->tuple_cell[u];
+        const int x = cell % c->W, y = cell / c->W;
+        members[(size_t)(y / TILE) * tx + x / TILE].push_back(u);
+    }
+    std::vector<int32_t> tile;
+    std::vector<uint16_t> rng;
+    std::vector<uint32_t> tup;
+    std::vector<int32_t> uidx;
+    for (const auto &m : members)
+        for (size_t c0 = 0; c0 < m.size(); c0 += CAP) {
+            const size_t n = std::min(m.size() - c0, (size_t)CAP);
+            tile.push_back((int32_t)uidx.size());
+            tile.push_back((int32_t)n);
+            std::vector<int> lo(P, 255), hi(P, 0);
+            for (size_t i = 0; i < n; i++) {
+                const int u = m[c0 + i];
+                uidx.push_back(u);
+                for (int w = 0; w < TW; w++)
+                    tup.push_back(c->tuples[(size_t)u * TW + w]);
+                for (int p = 0; p < P; p++) {
+                    const int l = (c->tuples[(size_t)u * TW + p / 4] >> (8 * (p & 3))) & 0xFF;
+                    lo[p] = std::min(lo[p], l);
+                    hi[p] = std::max(hi[p], l);
+                }
+            }
+            for (int p = 0; p < P; p++)
+                rng.push_back((uint16_t)(lo[p] | (hi[p] << 8)));
+        }
+    const int NT = (int)tile.size() / 2;
+    c->bb_NT = NT;
+    auto put = [&](const void *src, size_t bytes) {
+        const size_t at = c->bb_img.size();
+        c->bb_img.resize(at + ((bytes + 15) & ~(size_t)15), 0);
+        memcpy(c->bb_img.data() + at, src, bytes);
+        return at;
+    };
+    c->bb_img.clear();
+    put(tile.data(), tile.size() * 4);
+    put(rng.data(), rng.size() * 2);
+    put(tup.data(), tup.size() * 4);
+    put(uidx.data(), uidx.size() * 4);
 }
 
 void free_device(tdoa_ctx *c)
@@ -308,6 +369,7 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_prior);
     (void)hipFree(c->d_tuples);
     (void)hipFree(c->d_tuple_cell);
+    (void)hipFree(c->d_bb);
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_p1k_img);
     c->d_p1k_img = nullptr;
@@ -590,6 +652,24 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     kp.height = cfg->height_offset;
     kp.tuples = c->d_tuples;
     kp.tuple_cell = c->d_tuple_cell;
+    kp.bb_NT = c->bb_NT;
+    if (kp.bb_NT > 0) {
+        if (hipMalloc(&c->d_bb, c->bb_img.size()) != hipSuccess ||
+            hipMemcpy(c->d_bb, c->bb_img.data(), c->bb_img.size(), hipMemcpyHostToDevice) !=
+                hipSuccess) {
+            free_device(c);
+            delete c;
+            return fail(TDOA_ERR_NOMEM, "uploading the grid tile tables failed");
+        }
+        const char *b = (const char *)c->d_bb;
+        const size_t a1 = ((size_t)kp.bb_NT * 8 + 15) & ~(size_t)15;
+        const size_t a2 = a1 + ((((size_t)kp.bb_NT * c->P * 2) + 15) & ~(size_t)15);
+        const size_t a3 = a2 + ((((size_t)c->U * c->TW * 4) + 15) & ~(size_t)15);
+        kp.bb_tile = (const int32_t *)b;
+        kp.bb_rng = (const uint16_t *)(b + a1);
+        kp.bb_tuples = (const uint32_t *)(b + a2);
+        kp.bb_uidx = (const int32_t *)(b + a3);
+    }
     *out = c;
     return TDOA_OK;
 }

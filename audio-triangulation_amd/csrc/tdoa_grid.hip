@@ -16,6 +16,7 @@
 
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 
 #include "tdoa_internal.h"
 
@@ -152,6 +153,201 @@ __global__ void __launch_bounds__(1024) k_grid(tdoa_kparams kp, tdoa_kout out,
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_grid_bb: the same solve (max L, first argmax tuple) by exact branch and
+// bound, one wave per frame.  The distinct tuples are regrouped by the 8 x 8
+// block of cells their first cell lies in (entries of <= 64 tuples, host
+// table, build_bb_tiles); an entry's bound is the sum over pairs, in the pair
+// order of L itself, of the weighted-score maximum over the entry's lag range
+// for that pair.  Floating-point addition is monotone in each operand, so the
+// bound is >= the L of every tuple of the entry, computed exactly as k_grid
+// computes it (0 + w_0 + w_1 + ...).  The wave evaluates the entry with the
+// largest bound, then every entry whose bound is not below the best L found
+// so far; an entry whose bound is below it cannot hold a tuple that reaches
+// the maximum, so the result (max L, smallest tuple index among equal L) is
+// k_grid's, bit for bit.  Worst case (flat scores): every entry is evaluated,
+// about k_grid's work plus the bounds.
+template <typename T>
+__device__ __forceinline__ T max_t(T a, T b);
+template <> __device__ __forceinline__ float max_t<float>(float a, float b) { return fmaxf(a, b); }
+template <> __device__ __forceinline__ int64_t max_t<int64_t>(int64_t a, int64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ float readlane_t(float v, int l)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ int64_t readlane_t(int64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <typename T, int TWC, int JT>
+__global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out,
+                                                  const T *__restrict__ weighted, int64_t B)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW, PK = P * K;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
+    int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
+    uint16_t *rng = (uint16_t *)(smem + (size_t)NT * 8);                      // [NT][P]
+    T *Wl = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15)) + (size_t)wave * PK;
+    for (int e = tid; e < 2 * NT; e += blockDim.x)
+        tiles[e] = kp.bb_tile[e];
+    for (int e = tid; e < NT * P; e += blockDim.x)
+        rng[e] = kp.bb_rng[e];
+    __syncthreads();
+
+    const T lowest = lowest_t<T>();
+    for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
+        __builtin_amdgcn_wave_barrier();  // the previous frame's reads of Wl come first
+        for (int e = lane; e < PK; e += 64)
+            Wl[e] = weighted[f * PK + e];
+        __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+        // entry bounds, lane-strided
+        T bt[JT];
+#pragma unroll
+        for (int j = 0; j < JT; j++) {
+            const int t = lane + 64 * j;
+            T b = lowest;
+            if (t < NT) {
+                b = 0;
+                for (int p = 0; p < P; p++) {
+                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                    const T *w = Wl + p * K;
+                    T m = w[lo];
+                    for (int k = lo + 1; k <= hi; k++)
+                        m = max_t<T>(m, w[k]);
+                    b += m;
+                }
+            }
+            bt[j] = b;
+        }
+        // seed: the entry of largest bound (first on ties; NaN bounds never win)
+        T sv = lowest;
+        int st = 0;
+#pragma unroll
+        for (int j = 0; j < JT; j++)
+            if (bt[j] > sv) {
+                sv = bt[j];
+                st = lane + 64 * j;
+            }
+        for (int m = 32; m >= 1; m >>= 1)
+            better_t(sv, st, (T)__shfl_xor(sv, m, 64), __shfl_xor(st, m, 64));
+        const int seed = __builtin_amdgcn_readfirstlane(st);
+
+        T best = lowest;
+        int bu = INT_MAX;
+        // evaluate one entry: one tuple per lane; tuples with L > lowest only
+        // (k_grid never records an L equal to its start value)
+        auto eval = [&](int t) {
+            const int start = tiles[2 * t], cnt = tiles[2 * t + 1];
+            T L = lowest;
+            int ui = INT_MAX;
+            if (lane < cnt) {
+                const int u = start + lane;
+                L = 0;
+#pragma unroll
+                for (int tw = 0; tw < TWC; tw++) {
+                    if (tw < TW) {
+                        const uint32_t word = kp.bb_tuples[(size_t)u * TW + tw];
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            const int p = 4 * tw + b;
+                            if (p < P)
+                                L += Wl[p * K + ((word >> (8 * b)) & 0xFFu)];
+                        }
+                    }
+                }
+                ui = kp.bb_uidx[u];
+            }
+            const bool win = L > lowest && (L > best || (L == best && ui < bu));
+            if (__ballot(win) == 0)
+                return;
+            T v = win ? L : lowest;
+            int vi = win ? ui : INT_MAX;
+            for (int m = 32; m >= 1; m >>= 1)
+                better_t(v, vi, (T)__shfl_xor(v, m, 64), __shfl_xor(vi, m, 64));
+            best = readlane_t(v, 0);
+            bu = __builtin_amdgcn_readfirstlane(vi);
+        };
+        if (NT > 0)
+            eval(seed);
+#pragma unroll
+        for (int j = 0; j < JT; j++) {
+            const int t = lane + 64 * j;
+            uint64_t mask = __ballot(t < NT && t != seed && !(bt[j] < best));
+            while (mask) {
+                const int l = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                if (!(readlane_t(bt[j], l) < best))  // the best may have risen since
+                    eval(l + 64 * j);
+            }
+        }
+        if (lane == 0) {
+            const int ui = (bu < 0 || bu >= kp.U) ? 0 : bu;  // every L compared false: tuple 0
+            const int cell = kp.tuple_cell[ui];
+            if (out.cell)
+                out.cell[f] = cell;
+            store_max_t<T>(out, f, best);
+            if (out.xy) {
+                const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+                out.xy[2 * f] = (float)(cx - kp.half_w) / kp.grid_scale;
+                out.xy[2 * f + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+            }
+        }
+    }
+}
+
+int g_grid_bb = -1;  // TDOA_GRID_BB=0: k_grid only (A/B)
+
+template <typename T, int TWC, int JT>
+int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
+              hipStream_t st)
+{
+    const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
+    const size_t per_wave = (size_t)kp.P * kp.K * sizeof(T);
+    int nw = (int)((150 * 1024 - table) / per_wave);
+    nw = nw > 16 ? 16 : nw;
+    const size_t lds = table + (size_t)nw * per_wave;
+    const void *kern = (const void *)k_grid_bb<T, TWC, JT>;
+    const int res = tdoa_resident_blocks(kern, nw * 64, lds);
+    int64_t grid = (B + nw - 1) / nw;
+    if (res > 0 && grid > res)
+        grid = res;
+    hipLaunchKernelGGL((k_grid_bb<T, TWC, JT>), dim3((unsigned)grid), dim3(nw * 64), lds, st, kp, out,
+                       weighted, B);
+    return 0;
+}
+
+template <typename T, int TWC>
+int launch_bb_jt(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
+                 hipStream_t st)
+{
+    switch ((kp.bb_NT + 63) / 64) {
+    case 1: return launch_bb<T, TWC, 1>(kp, out, weighted, B, st);
+    case 2: return launch_bb<T, TWC, 2>(kp, out, weighted, B, st);
+    case 3: return launch_bb<T, TWC, 3>(kp, out, weighted, B, st);
+    default: return launch_bb<T, TWC, 4>(kp, out, weighted, B, st);
+    }
+}
+
+// k_grid_bb applies: tables built, at most 256 entries, and room for the
+// entry table plus one frame's scores
+template <typename T>
+bool bb_fits(const tdoa_kparams &kp)
+{
+    if (g_grid_bb < 0) {
+        const char *s = getenv("TDOA_GRID_BB");
+        g_grid_bb = s ? atoi(s) : 1;
+    }
+    if (!g_grid_bb || kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
+        return false;
+    const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
+    return table + (size_t)kp.P * kp.K * sizeof(T) <= 150 * 1024;
+}
+
 int hip_fail(hipError_t e, const char *what)
 {
     char buf[256];
@@ -203,6 +399,14 @@ int launch(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int6
         return tdoa_set_error(-1, "grid: batch too large for one launch");
     hipStream_t st = (hipStream_t)stream;
     constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
+    if (bb_fits<T>(kp)) {
+        if (kp.TW == 1)
+            launch_bb_jt<T, 1>(kp, out, weighted, B, st);
+        else
+            launch_bb_jt<T, TWX>(kp, out, weighted, B, st);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "k_grid_bb launch");
+    }
     if (kp.TW == 1)
         launch_gf<T, 1>(gf, dim3((unsigned)grid), dim3(threads), lds, st, kp, out, weighted, B, CH);
     else

@@ -47,6 +47,14 @@ struct tdoa_kparams {
     const uint8_t *lut;        // [P][G] lag index per cell (heat map)
     const void *p1k_img;       // config-2 GCC-PHAT kernel: its LDS table image (16-B units)
     int32_t p1k_img_bytes;
+    // exact branch-and-bound grid (k_grid_bb): the distinct tuples regrouped
+    // by the 8 x 8-cell tile of their first cell (<= 64 tuples per entry);
+    // per entry and pair the lag range [lo, hi] of its tuples
+    int32_t bb_NT;             // tile entries (0: no table, k_grid only)
+    const int32_t *bb_tile;    // [NT][2] first tuple (regrouped order), count
+    const uint16_t *bb_rng;    // [NT][P] lo | hi << 8
+    const uint32_t *bb_tuples; // [U][TW] regrouped tuples
+    const int32_t *bb_uidx;    // [U] their index in first-cell order
     // least-squares refinement (tdoa_ls.hip)
     const float *mic_xy;       // [M][2] metres
     float fs, c, height;

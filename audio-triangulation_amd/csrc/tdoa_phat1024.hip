@@ -78,6 +78,73 @@ __device__ __forceinline__ float dpp_xor1(float v)
 __device__ __forceinline__ f2 dpp_xor1(f2 v) { return f2{dpp_xor1(v.x), dpp_xor1(v.y)}; }
 typedef short v2s_t __attribute__((ext_vector_type(2)));
 
+// Partner swap of the upper 16 bins (registers 16..31), exec-masked instead of
+// two selects per dword: lanes other than 0, 1 (of each half-wave) take their
+// DPP partner's register in place (one instruction per dword); lane 0 then
+// shifts its own upper half by one register (FWD: V[j] <- V[j+1], V[31] <- V[0];
+// !FWD: V[j] <- V[j-1], V[16] <- E) in 64-bit moves; lane 1 keeps its registers.
+// Wait states inside the strings: 2 before a DPP reads a VGPR a VALU wrote
+// (s_nop 1; the compiler pads only its own boundary), and a conservative
+// s_nop 4 after each EXEC write ahead of a DPP / VALU.
+#define P1K_X(i) "%" #i
+#define P1K_DPP(i) "v_mov_b32_dpp " P1K_X(i) ", " P1K_X(i) " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+#define P1K_MOV(d, s) "v_mov_b64 " P1K_X(d) ", " P1K_X(s) "\n\t"
+template <bool FWD, int NV>
+__device__ __forceinline__ void swap_upper_exec(f2 (&V)[NV], f2 E)
+{
+    float x[32];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        x[2 * j] = V[16 + j].x;
+        x[2 * j + 1] = V[16 + j].y;
+    }
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_and_b64 exec, exec, %[m1]\n\t"
+                 "s_nop 4\n\t" P1K_DPP(0) P1K_DPP(1) P1K_DPP(2) P1K_DPP(3) P1K_DPP(4) P1K_DPP(5)
+                     P1K_DPP(6) P1K_DPP(7) P1K_DPP(8) P1K_DPP(9) P1K_DPP(10) P1K_DPP(11) P1K_DPP(12)
+                         P1K_DPP(13) P1K_DPP(14) P1K_DPP(15) P1K_DPP(16) P1K_DPP(17) P1K_DPP(18)
+                             P1K_DPP(19) P1K_DPP(20) P1K_DPP(21) P1K_DPP(22) P1K_DPP(23) P1K_DPP(24)
+                                 P1K_DPP(25) P1K_DPP(26) P1K_DPP(27) P1K_DPP(28) P1K_DPP(29)
+                                     P1K_DPP(30) P1K_DPP(31) "s_mov_b64 exec, %[sv]\n\t"
+                 "s_nop 4"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                   "+v"(x[6]), "+v"(x[7]), "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]),
+                   "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]), "+v"(x[16]), "+v"(x[17]),
+                   "+v"(x[18]), "+v"(x[19]), "+v"(x[20]), "+v"(x[21]), "+v"(x[22]), "+v"(x[23]),
+                   "+v"(x[24]), "+v"(x[25]), "+v"(x[26]), "+v"(x[27]), "+v"(x[28]), "+v"(x[29]),
+                   "+v"(x[30]), "+v"(x[31]), [sv] "=&s"(sv)
+                 : [m1] "s"(0xFFFFFFFCFFFFFFFCull));
+    f2 y[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        y[j] = f2{x[2 * j], x[2 * j + 1]};
+    const f2 e = FWD ? V[0] : E;
+#define P1K_ROT_ASM(ROT)                                                                            \
+    asm volatile("s_mov_b64 %[sv], exec\n\t"                                                        \
+                 "s_and_b64 exec, exec, %[m2]\n\t"                                                  \
+                 "s_nop 4\n\t" ROT "s_mov_b64 exec, %[sv]\n\t"                                     \
+                 "s_nop 4"                                                                           \
+                 : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]),           \
+                   "+v"(y[6]), "+v"(y[7]), "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]),         \
+                   "+v"(y[12]), "+v"(y[13]), "+v"(y[14]), "+v"(y[15]), [sv] "=&s"(sv)                \
+                 : [m2] "s"(0x0000000100000001ull), [e] "v"(e))
+    if constexpr (FWD)
+        P1K_ROT_ASM(P1K_MOV(0, 1) P1K_MOV(1, 2) P1K_MOV(2, 3) P1K_MOV(3, 4) P1K_MOV(4, 5) P1K_MOV(5, 6)
+                        P1K_MOV(6, 7) P1K_MOV(7, 8) P1K_MOV(8, 9) P1K_MOV(9, 10) P1K_MOV(10, 11)
+                            P1K_MOV(11, 12) P1K_MOV(12, 13) P1K_MOV(13, 14) P1K_MOV(14, 15)
+                                "v_mov_b64 %15, %[e]\n\t");
+    else
+        P1K_ROT_ASM(P1K_MOV(15, 14) P1K_MOV(14, 13) P1K_MOV(13, 12) P1K_MOV(12, 11) P1K_MOV(11, 10)
+                        P1K_MOV(10, 9) P1K_MOV(9, 8) P1K_MOV(8, 7) P1K_MOV(7, 6) P1K_MOV(6, 5)
+                            P1K_MOV(5, 4) P1K_MOV(4, 3) P1K_MOV(3, 2) P1K_MOV(2, 1) P1K_MOV(1, 0)
+                                "v_mov_b64 %0, %[e]\n\t");
+#undef P1K_ROT_ASM
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        V[16 + j] = y[j];
+}
+
 __device__ __forceinline__ void better(float &bv, int &bu, float ov, int ou)
 {
     if (ov > bv || (ov == bv && ou < bu)) {
@@ -737,12 +804,16 @@ __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)
     fft_col_lds<false, true>(L, v, L.tileA);
     fft_row_fwd(L, L.tileA, V);
     V[32] = c_unit(conjf2(V[16]), e2);
+#ifdef P1K_SELECT_SWAP
 #pragma unroll
     for (int j = 16; j < 32; j++) {
         const f2 t = dpp_xor1(V[j]);
         const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
         V[j] = (L.is0 || L.is1) ? own : t;
     }
+#else
+    swap_upper_exec<true>(V, f2{0.0f, 0.0f});
+#endif
 }
 
 // real-FFT split of the partner pair k + unit normalisation: the unit
@@ -877,12 +948,16 @@ __device__ __forceinline__ void lean_pretwiddle(const Lane &L, const f2 (&A)[33]
     }
     const f2 R32 = CROSS ? c_conjmul(A[32], Bs[32]) : A[32];
     const f2 Ye = f2{2.0f * R32.x, -2.0f * R32.y};  // Y[512] = 2 conj(R[512])
+#ifdef P1K_SELECT_SWAP
 #pragma unroll
     for (int j = 31; j >= 16; j--) {
         const f2 t = dpp_xor1(v[j]);
         const f2 own = L.is0 ? (j == 16 ? Ye : v[j - 1]) : v[j];
         v[j] = (L.is0 || L.is1) ? own : t;
     }
+#else
+    swap_upper_exec<false>(v, Ye);
+#endif
 }
 
 }  // namespace

@@ -222,3 +222,29 @@ def test_grid_exact_on_own_scores(phat3, kind):
     cell, mx = _grid_f32(got["weighted_f"], lut)
     assert (got["cell"] == cell).all()
     assert (got["max_Lf"] == mx).all()
+
+
+@pytest.mark.parametrize("shape", ["cfg3", "cfg4"])
+@pytest.mark.parametrize("kind", ["adc", "noise_only", "constant"])
+def test_grid_bb_exact_on_own_scores(shape, kind):
+    """Configs 3/4 solve the grid by exact branch and bound (k_grid_bb: entries
+    of <= 64 tuples from one 8 x 8 block of cells, skipped when their bound is
+    below the best L found).  Cell and max L must equal the exhaustive float32
+    scan of the engine's own weighted scores bit for bit: peaked scores (ADC
+    frames, strong pruning), flat noisy scores (weak bounds) and all-equal
+    scores (every entry ties: first cell)."""
+    M, N, xy = (4, 4096, synth.square_mics(0.15)) if shape == "cfg3" else (8, 2048, synth.circle_mics(8, 0.15))
+    loc = Localizer(engine="gcc_phat", num_mics=M, frame_len=N, mic_xy=xy)
+    lut = loc.lut()
+    B = 300
+    if kind == "adc":
+        fr, _, _ = synth.adc_frames(B, M, N, lut.reshape(-1, 101, 101), loc.dims.S, 91, device="cuda")
+    elif kind == "noise_only":
+        g = torch.Generator(device="cpu").manual_seed(6)
+        fr = torch.randint(0, 256, (B, M, N), generator=g, dtype=torch.int16).cuda()
+    else:
+        fr = torch.full((8, M, N), 77, dtype=torch.int16, device="cuda")
+    got = _np(loc.localize(fr, scores=True))
+    cell, mx = _grid_f32(got["weighted_f"], lut)
+    assert (got["cell"] == cell).all()
+    assert (got["max_Lf"] == mx).all()

@@ -14,6 +14,8 @@
 #   sq[:CFG[:ENGINE]]     two SQ counter passes (waves, VALU, LDS, waits)
 #   pmcx:CFG:ENGINE:NAME:C1,C2,..  one pass of the listed counters (mind the
 #                         per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
+#   ablib[:L1,L2,..]      bench config 2 once per library tdoa/<L>.so (TDOA_LIB)
+#   testlib:L[:FILES]     pytest -m gpu against tdoa/<L>.so
 #   smoke                 __graft_entry__.smoke()
 #
 # Env: TAG (output subdirectory, default "cur"), STEPS (bench steps),
@@ -58,6 +60,25 @@ for step in "$@"; do
                 $BENCH_ARGS > "$OUT/ab_$w.log" 2>&1 || { echo "bench $w failed"; tail -5 "$OUT/ab_$w.log"; exit 21; }
             tail -1 "$OUT/ab_$w.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('WAVES=$w value %.4g kernel_ms %.4f frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))"
         done
+        ;;
+    ablib)
+        # bench config 2 once per library variant (audio-triangulation_amd/tdoa/<name>.so)
+        vs=$(field "$step" 2 "libtdoa,libtdoa_alt")
+        for l in ${vs//,/ }; do
+            TDOA_LIB=$ROOT/audio-triangulation_amd/tdoa/$l.so timeout -k 10 240 python bench.py --steps ${STEPS:-400} \
+                --no-cpu $BENCH_ARGS > "$OUT/ablib_$l.log" 2>&1 || { echo "bench $l failed"; tail -5 "$OUT/ablib_$l.log"; exit 21; }
+            tail -1 "$OUT/ablib_$l.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$l value %.4g kernel_ms %.4f frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))"
+        done
+        ;;
+    testlib)
+        # pytest -m gpu of FILES against library variant LIB: testlib:LIB:FILES
+        l=$(field "$step" 2 libtdoa_alt); files=$(field "$step" 3 tests)
+        files=${files//,/ }
+        TDOA_LIB=$ROOT/audio-triangulation_amd/tdoa/$l.so timeout -k 10 900 python -u -m pytest $files -m gpu -x -q \
+            --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_$l.log" 2>&1
+        rc=$?
+        grep -E "passed|failed|error" "$OUT/pytest_$l.log" | tail -3
+        [ $rc -ne 0 ] && { tail -30 "$OUT/pytest_$l.log"; exit $rc; }
         ;;
     bench)
         c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
