@@ -192,7 +192,8 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
     int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
     uint16_t *rng = (uint16_t *)(smem + (size_t)NT * 8);                      // [NT][P]
-    T *Wl = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15)) + (size_t)wave * PK;
+    T *Wl = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15)) + (size_t)wave * (PK + 128);
+    T *M8 = Wl + PK;  // [K] running maxima of one pair (K <= 127)
     for (int e = tid; e < 2 * NT; e += blockDim.x)
         tiles[e] = kp.bb_tile[e];
     for (int e = tid; e < NT * P; e += blockDim.x)
@@ -205,24 +206,56 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
         for (int e = lane; e < PK; e += 64)
             Wl[e] = weighted[f * PK + e];
         __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
-        // entry bounds, lane-strided
+        // entry bounds, lane-strided, pair by pair in L's own order: for pair
+        // p the wave builds the 8-wide running maxima M8[k] = max w[k..k+7]
+        // (clamped to K - 1) in its scratch row; a range [lo, hi] of width
+        // <= 16 is then max(M8[lo], M8[max(lo, hi - 7)]) -- two independent
+        // reads instead of a dependent chain (wider ranges loop by 8)
         T bt[JT];
 #pragma unroll
-        for (int j = 0; j < JT; j++) {
-            const int t = lane + 64 * j;
-            T b = lowest;
-            if (t < NT) {
-                b = 0;
-                for (int p = 0; p < P; p++) {
-                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                    const T *w = Wl + p * K;
-                    T m = w[lo];
-                    for (int k = lo + 1; k <= hi; k++)
-                        m = max_t<T>(m, w[k]);
-                    b += m;
+        for (int j = 0; j < JT; j++)
+            bt[j] = (lane + 64 * j < NT) ? (T)0 : lowest;
+        if (P <= 8) {  // few pairs: the M8 rows cost more than they save
+#pragma unroll
+            for (int j = 0; j < JT; j++) {
+                const int t = lane + 64 * j;
+                if (t < NT) {
+                    T b = 0;
+                    for (int p = 0; p < P; p++) {
+                        const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                        const T *w = Wl + p * K;
+                        T m = w[lo];
+                        for (int k = lo + 1; k <= hi; k++)
+                            m = max_t<T>(m, w[k]);
+                        b += m;
+                    }
+                    bt[j] = b;
                 }
             }
-            bt[j] = b;
+        } else
+        for (int p = 0; p < P; p++) {
+            const T *w = Wl + p * K;
+            __builtin_amdgcn_wave_barrier();  // previous pair's M8 reads come first
+            for (int k = lane; k < K; k += 64) {
+                T m = w[k];
+#pragma unroll
+                for (int d = 1; d < 8; d++)
+                    m = max_t<T>(m, w[k + d < K ? k + d : K - 1]);
+                M8[k] = m;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < JT; j++) {
+                const int t = lane + 64 * j;
+                if (t < NT) {
+                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                    T m = M8[lo];
+                    for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
+                        m = max_t<T>(m, M8[k]);
+                    m = max_t<T>(m, M8[hi - 7 > lo ? hi - 7 : lo]);
+                    bt[j] += m;
+                }
+            }
         }
         // seed: the entry of largest bound (first on ties; NaN bounds never win)
         T sv = lowest;
@@ -307,7 +340,7 @@ int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, i
               hipStream_t st)
 {
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
-    const size_t per_wave = (size_t)kp.P * kp.K * sizeof(T);
+    const size_t per_wave = ((size_t)kp.P * kp.K + 128) * sizeof(T);
     int nw = (int)((150 * 1024 - table) / per_wave);
     nw = nw > 16 ? 16 : nw;
     const size_t lds = table + (size_t)nw * per_wave;
@@ -345,7 +378,7 @@ bool bb_fits(const tdoa_kparams &kp)
     if (!g_grid_bb || kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
         return false;
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
-    return table + (size_t)kp.P * kp.K * sizeof(T) <= 150 * 1024;
+    return kp.K <= 127 && table + ((size_t)kp.P * kp.K + 128) * sizeof(T) <= 150 * 1024;
 }
 
 int hip_fail(hipError_t e, const char *what)

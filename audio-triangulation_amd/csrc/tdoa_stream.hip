@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include "tdoa_internal.h"
 
@@ -357,6 +358,200 @@ __global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp,
     }
 }
 
+// Persistent form of k_stream_trigger_w (same scan, same results): each wave
+// walks streams gw, gw + GW, ... with the NEXT stream's capture words and ring
+// start already requested while it scans the current one (the one-stream-per-
+// wave kernel waited on its loads at the start of every wave: 68 % of wave
+// cycles in SQ_WAIT_ANY).  A firing stream's frame is written from the words
+// the wave already holds, staged through LDS (no second read of the ring).
+template <int G, int M>
+__global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
+{
+    constexpr int H = 64 * G, N = 2 * H, CB = G * M, CW = CB / 4;
+    static_assert(CB % 4 == 0, "a lane's chunk is whole words");
+    extern __shared__ __attribute__((aligned(16))) uint32_t stage_all[];  // [4 waves][3 H M / 4]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t *stage = stage_all + wv * (3 * H * M / 4);
+    const int64_t GW = (int64_t)gridDim.x * 4;
+    int64_t s = (int64_t)blockIdx.x * 4 + wv;
+    if (s >= S)
+        return;  // whole wave: no workgroup barrier below
+    const int64_t pos = *sp.pos;
+    const int64_t base = pos + 1 - N;
+    const int64_t cl = sp.capture_len;
+    int64_t j0 = base % cl;
+    if (j0 < 0)
+        j0 += cl;
+    // ring positions of the lane's three chunks: the same for every stream
+    int64_t jr[3];
+    bool fast[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int64_t l0 = base + r * H + G * lane;
+        int64_t j = j0 + r * H + G * lane;
+        if (j >= cl)
+            j -= cl;
+        jr[r] = j;
+        fast[r] = l0 >= 0 && (j + G) * M + 7 <= cl * M;
+    }
+    // aligned words of the fast rows (the word pointer and the byte shift from
+    // the absolute address: a ring need not start 4-byte aligned)
+    auto fetch = [&](int64_t st, uint32_t (&w)[3][CW + 1], uint32_t (&sh)[3]) {
+        const uint8_t *cap = sp.capture + (size_t)st * cl * M;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const uintptr_t p = (uintptr_t)(cap + (size_t)(fast[r] ? jr[r] : 0) * M);
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(p & ~(uintptr_t)3);
+            sh[r] = (uint32_t)(p & 3u);
+#pragma unroll
+            for (int k = 0; k <= CW; k++)
+                w[r][k] = fast[r] ? wp[k] : 0u;
+        }
+    };
+    uint32_t wc[3][CW + 1], shc[3];
+    fetch(s, wc, shc);
+    int64_t rs = sp.ring_start[s];
+    constexpr int hb = __builtin_ctz(N) - 1;
+    const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
+    for (;;) {
+        const uint8_t *cap = sp.capture + (size_t)s * cl * M;
+        uint32_t x[3][CW];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            if (fast[r]) {
+#pragma unroll
+                for (int k = 0; k < CW; k++)
+                    x[r][k] = __builtin_amdgcn_alignbyte(wc[r][k + 1], wc[r][k], shc[r]);
+            } else {  // stream start (zeros) or the ring's end
+                const int64_t l0 = base + r * H + G * lane;
+#pragma unroll
+                for (int k = 0; k < CW; k++)
+                    x[r][k] = 0;
+#pragma unroll
+                for (int i = 0; i < G; i++) {
+                    int64_t ji = jr[r] + i;
+                    if (ji >= cl)
+                        ji -= cl;
+#pragma unroll
+                    for (int m = 0; m < M; m++) {
+                        const int b = i * M + m;
+                        const uint32_t v = l0 + i < 0 ? 0u : (uint32_t)cap[(size_t)ji * M + m];
+                        x[r][b >> 2] |= v << (8 * (b & 3));
+                    }
+                }
+            }
+        }
+        // the next stream's words into the same registers, in flight while
+        // this stream is scanned
+        const int64_t sn = s + GW;
+        int64_t rsn = 0;
+        if (sn < S) {
+            fetch(sn, wc, shc);
+            rsn = sp.ring_start[sn];
+        }
+        auto smp = [&](int r, int i, int m) -> int {
+            const int b = i * M + m;
+            return (int)((x[r][b >> 2] >> (8 * (b & 3))) & 0xFFu);
+        };
+        int q1[3][M], q2[3];
+        {
+            int tot1[M], tot2 = 0;
+#pragma unroll
+            for (int m = 0; m < M; m++)
+                tot1[m] = 0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                int c2 = 0;
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    int c1 = 0;
+#pragma unroll
+                    for (int i = 0; i < G; i++) {
+                        const int v = smp(r, i, m);
+                        c1 += v;
+                        c2 += v * v;
+                    }
+                    const int inc = wave_scan_incl(c1);
+                    q1[r][m] = tot1[m] + inc - c1;
+                    tot1[m] += __builtin_amdgcn_readlane(inc, 63);
+                }
+                const int inc2 = wave_scan_incl(c2);
+                q2[r] = tot2 + inc2 - c2;
+                tot2 += __builtin_amdgcn_readlane(inc2, 63);
+            }
+        }
+        // the words re-enter here opaque: the scan re-extracts the samples
+        // instead of keeping the prefix pass's 3 G M extracted bytes live
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int k = 0; k < CW; k++)
+                asm volatile("" : "+v"(x[r][k]));
+        const int64_t amin = rs + N - pos - 1;  // full ring: >= N samples since the last trigger
+        int fi = -1;
+#pragma unroll
+        for (int i = 0; i < G; i++) {
+            const int a = G * lane + i;
+            long long pout = (long long)(q2[1] - q2[0]) << hb, pin = (long long)(q2[2] - q2[1]) << hb;
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                const long long so1 = q1[1][m] - q1[0][m], si1 = q1[2][m] - q1[1][m];
+                pout -= so1 * so1;
+                pin -= si1 * si1;
+            }
+            if (fi < 0 && a >= amin && pout > thr + pin)
+                fi = i;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    const int v = smp(r, i, m);
+                    q1[r][m] += v;
+                    q2[r] += v * v;
+                }
+            }
+        }
+        const uint64_t fire = __ballot(fi >= 0);
+        if (fire != 0) {
+            const int fl = __builtin_ctzll(fire);  // lowest lane = lowest candidates
+            const int a = G * fl + __builtin_amdgcn_readlane(fi, fl);
+            int slot = 0;
+            if (lane == 0) {
+                slot = atomicAdd(sp.count, 1);
+                const int64_t end = pos + 1 + a;
+                sp.ids[slot] = (int32_t)s;
+                sp.end[slot] = end;
+                sp.ring_start[s] = end;
+            }
+            slot = __builtin_amdgcn_readfirstlane(slot);
+            // the frame (local samples a .. a + N - 1 of every mic, rolling_buffer.c:48-62
+            // order) from the words in registers: rows 0..2 staged as [l][m] bytes
+            __builtin_amdgcn_wave_barrier();  // the previous stream's stage reads come first
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int k = 0; k < CW; k++)
+                    stage[r * (H * M / 4) + lane * CW + k] = x[r][k];
+            __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+            const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
+            int16_t *dst = sp.frames + (size_t)slot * M * N;
+#pragma unroll 4
+            for (int t = 0; t < N / 64; t++) {
+                const int n = lane + 64 * t;
+#pragma unroll
+                for (int m = 0; m < M; m++)
+                    dst[(size_t)m * N + n] = (int16_t)sb[(a + n) * M + m];
+            }
+        }
+        if (sn >= S)
+            break;
+        s = sn;
+        rs = rsn;
+    }
+}
+
+int g_trigger_p = -1;  // TDOA_TRIGGER_P=0: one stream per wave (k_stream_trigger_w)
+
 // correlations.c:40-43 in the reference's float/double steps
 __device__ __forceinline__ float decay_us(uint64_t now, uint64_t last)
 {
@@ -549,9 +744,35 @@ size_t tdoa_stream_trigger_lds(int M, int N, int H)
     return ((M * L * 2 + 15) & ~(size_t)15) + (((L + 1) * 4 + 15) & ~(size_t)15) + (L + 1) * 8;
 }
 
+template <int G, int M>
+static void launch_trigger_p(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+{
+    const size_t lds = (size_t)4 * 3 * 64 * G * M;
+    const int res = tdoa_resident_blocks((const void *)k_stream_trigger_p<G, M>, 256, lds);
+    int64_t grid = (S + 3) / 4;
+    if (res > 0 && grid > res)
+        grid = res;
+    hipLaunchKernelGGL((k_stream_trigger_p<G, M>), dim3((unsigned)grid), dim3(256), lds, st, sp, S);
+}
+
 template <int G>
 static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
 {
+    if (g_trigger_p < 0) {
+        const char *e = getenv("TDOA_TRIGGER_P");
+        g_trigger_p = e ? atoi(e) : 1;
+    }
+    if (g_trigger_p) {
+        if (sp.M == 2)
+            launch_trigger_p<G, 2>(sp, S, st);
+        else if (sp.M == 3)
+            launch_trigger_p<G, 3>(sp, S, st);
+        else if (sp.M == 4)
+            launch_trigger_p<G, 4>(sp, S, st);
+        else
+            return false;
+        return true;
+    }
     const dim3 grid((unsigned)((S + 3) / 4));
     if (sp.M == 2)
         hipLaunchKernelGGL((k_stream_trigger_w<G, 2>), grid, dim3(256), 0, st, sp, S);
