@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "tdoa_internal.h"
+#include "tdoa_grid_bb.h"
 
 int tdoa_set_error(int code, const char *msg);
 
@@ -155,40 +156,13 @@ __global__ void __launch_bounds__(1024) k_grid(tdoa_kparams kp, tdoa_kout out,
 
 // ---------------------------------------------------------------------------
 // k_grid_bb: the same solve (max L, first argmax tuple) by exact branch and
-// bound, one wave per frame.  The distinct tuples are regrouped by the 8 x 8
-// block of cells their first cell lies in (entries of <= 64 tuples, host
-// table, build_bb_tiles); an entry's bound is the sum over pairs, in the pair
-// order of L itself, of the weighted-score maximum over the entry's lag range
-// for that pair.  Floating-point addition is monotone in each operand, so the
-// bound is >= the L of every tuple of the entry, computed exactly as k_grid
-// computes it (0 + w_0 + w_1 + ...).  The wave evaluates the entry with the
-// largest bound, then every entry whose bound is not below the best L found
-// so far; an entry whose bound is below it cannot hold a tuple that reaches
-// the maximum, so the result (max L, smallest tuple index among equal L) is
-// k_grid's, bit for bit.  Worst case (flat scores): every entry is evaluated,
-// about k_grid's work plus the bounds.
-template <typename T>
-__device__ __forceinline__ T max_t(T a, T b);
-template <> __device__ __forceinline__ float max_t<float>(float a, float b) { return fmaxf(a, b); }
-template <> __device__ __forceinline__ int64_t max_t<int64_t>(int64_t a, int64_t b) { return a > b ? a : b; }
-
-__device__ __forceinline__ float readlane_t(float v, int l)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-__device__ __forceinline__ int64_t readlane_t(int64_t v, int l)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
+// bound, one wave per frame (tdoa_grid_bb.h).
 template <typename T, int TWC, int JT>
 __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out,
                                                   const T *__restrict__ weighted, int64_t B)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW, PK = P * K;
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, PK = P * K;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
     int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
     uint16_t *rng = (uint16_t *)(smem + (size_t)NT * 8);                      // [NT][P]
@@ -200,124 +174,14 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
         rng[e] = kp.bb_rng[e];
     __syncthreads();
 
-    const T lowest = lowest_t<T>();
     for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
         __builtin_amdgcn_wave_barrier();  // the previous frame's reads of Wl come first
         for (int e = lane; e < PK; e += 64)
             Wl[e] = weighted[f * PK + e];
         __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
-        // entry bounds, lane-strided, pair by pair in L's own order: for pair
-        // p the wave builds the 8-wide running maxima M8[k] = max w[k..k+7]
-        // (clamped to K - 1) in its scratch row; a range [lo, hi] of width
-        // <= 16 is then max(M8[lo], M8[max(lo, hi - 7)]) -- two independent
-        // reads instead of a dependent chain (wider ranges loop by 8)
-        T bt[JT];
-#pragma unroll
-        for (int j = 0; j < JT; j++)
-            bt[j] = (lane + 64 * j < NT) ? (T)0 : lowest;
-        if (P <= 8) {  // few pairs: the M8 rows cost more than they save
-#pragma unroll
-            for (int j = 0; j < JT; j++) {
-                const int t = lane + 64 * j;
-                if (t < NT) {
-                    T b = 0;
-                    for (int p = 0; p < P; p++) {
-                        const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                        const T *w = Wl + p * K;
-                        T m = w[lo];
-                        for (int k = lo + 1; k <= hi; k++)
-                            m = max_t<T>(m, w[k]);
-                        b += m;
-                    }
-                    bt[j] = b;
-                }
-            }
-        } else
-        for (int p = 0; p < P; p++) {
-            const T *w = Wl + p * K;
-            __builtin_amdgcn_wave_barrier();  // previous pair's M8 reads come first
-            for (int k = lane; k < K; k += 64) {
-                T m = w[k];
-#pragma unroll
-                for (int d = 1; d < 8; d++)
-                    m = max_t<T>(m, w[k + d < K ? k + d : K - 1]);
-                M8[k] = m;
-            }
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int j = 0; j < JT; j++) {
-                const int t = lane + 64 * j;
-                if (t < NT) {
-                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                    T m = M8[lo];
-                    for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
-                        m = max_t<T>(m, M8[k]);
-                    m = max_t<T>(m, M8[hi - 7 > lo ? hi - 7 : lo]);
-                    bt[j] += m;
-                }
-            }
-        }
-        // seed: the entry of largest bound (first on ties; NaN bounds never win)
-        T sv = lowest;
-        int st = 0;
-#pragma unroll
-        for (int j = 0; j < JT; j++)
-            if (bt[j] > sv) {
-                sv = bt[j];
-                st = lane + 64 * j;
-            }
-        for (int m = 32; m >= 1; m >>= 1)
-            better_t(sv, st, (T)__shfl_xor(sv, m, 64), __shfl_xor(st, m, 64));
-        const int seed = __builtin_amdgcn_readfirstlane(st);
-
-        T best = lowest;
-        int bu = INT_MAX;
-        // evaluate one entry: one tuple per lane; tuples with L > lowest only
-        // (k_grid never records an L equal to its start value)
-        auto eval = [&](int t) {
-            const int start = tiles[2 * t], cnt = tiles[2 * t + 1];
-            T L = lowest;
-            int ui = INT_MAX;
-            if (lane < cnt) {
-                const int u = start + lane;
-                L = 0;
-#pragma unroll
-                for (int tw = 0; tw < TWC; tw++) {
-                    if (tw < TW) {
-                        const uint32_t word = kp.bb_tuples[(size_t)u * TW + tw];
-#pragma unroll
-                        for (int b = 0; b < 4; b++) {
-                            const int p = 4 * tw + b;
-                            if (p < P)
-                                L += Wl[p * K + ((word >> (8 * b)) & 0xFFu)];
-                        }
-                    }
-                }
-                ui = kp.bb_uidx[u];
-            }
-            const bool win = L > lowest && (L > best || (L == best && ui < bu));
-            if (__ballot(win) == 0)
-                return;
-            T v = win ? L : lowest;
-            int vi = win ? ui : INT_MAX;
-            for (int m = 32; m >= 1; m >>= 1)
-                better_t(v, vi, (T)__shfl_xor(v, m, 64), __shfl_xor(vi, m, 64));
-            best = readlane_t(v, 0);
-            bu = __builtin_amdgcn_readfirstlane(vi);
-        };
-        if (NT > 0)
-            eval(seed);
-#pragma unroll
-        for (int j = 0; j < JT; j++) {
-            const int t = lane + 64 * j;
-            uint64_t mask = __ballot(t < NT && t != seed && !(bt[j] < best));
-            while (mask) {
-                const int l = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                if (!(readlane_t(bt[j], l) < best))  // the best may have risen since
-                    eval(l + 64 * j);
-            }
-        }
+        T best;
+        int bu;
+        tdoa_bb::solve_wave<T, TWC, JT>(kp, Wl, M8, tiles, rng, lane, best, bu);
         if (lane == 0) {
             const int ui = (bu < 0 || bu >= kp.U) ? 0 : bu;  // every L compared false: tuple 0
             const int cell = kp.tuple_cell[ui];

@@ -1,0 +1,185 @@
+// tdoa_grid_bb.h -- the exact branch-and-bound grid solve of one frame by one
+// wave (vga_heatmap.h:99-108: max L over cells, first row-major argmax),
+// shared by k_grid_bb (tdoa_grid.hip) and the streaming update
+// (tdoa_stream.hip).  See DESIGN.md "k_grid_bb".
+//
+// The distinct tuples are regrouped by the 8 x 8 block of cells their first
+// cell lies in (entries of <= 64 tuples, host table, build_bb_tiles); an
+// entry's bound is the sum over pairs, in the pair order of L itself, of the
+// weighted-score maximum over the entry's lag range for that pair.  Addition
+// (float or int64) is monotone in each operand, so the bound is >= the L of
+// every tuple of the entry, computed exactly as the exhaustive scan computes it
+// (0 + w_0 + w_1 + ...).  The wave evaluates the entry with the largest bound,
+// then every entry whose bound is not below the best L found so far; an entry
+// whose bound is below it cannot hold a tuple that reaches the maximum, so the
+// result (max L, smallest tuple index among equal L) is the exhaustive scan's,
+// bit for bit.  Worst case (flat scores): every entry is evaluated.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+#include <cmath>
+
+#include "tdoa_internal.h"
+
+namespace tdoa_bb {
+
+template <typename T> __device__ __forceinline__ T lowest();
+template <> __device__ __forceinline__ int64_t lowest<int64_t>() { return INT64_MIN; }
+template <> __device__ __forceinline__ float lowest<float>() { return -INFINITY; }
+
+template <typename T> __device__ __forceinline__ T vmax(T a, T b);
+template <> __device__ __forceinline__ float vmax<float>(float a, float b) { return fmaxf(a, b); }
+template <> __device__ __forceinline__ int64_t vmax<int64_t>(int64_t a, int64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ float readlane(float v, int l)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ int64_t readlane(int64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <typename T>
+__device__ __forceinline__ void better(T &bv, int &bu, T ov, int ou)
+{
+    if (ov > bv || (ov == bv && ou < bu)) {
+        bv = ov;
+        bu = ou;
+    }
+}
+
+// One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
+// by this wave before the call); M8: a [128] LDS scratch row of this wave;
+// tiles / rng: the entry table (LDS or global).  Returns the max L (best) and
+// its tuple index in first-cell order (bu, INT_MAX when no L exceeded the
+// lowest value).  Every lane returns the same pair.
+template <typename T, int TWC, int JT>
+__device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, T *M8,
+                                           const int32_t *tiles, const uint16_t *rng, int lane,
+                                           T &best_out, int &bu_out)
+{
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW;
+    const T low = lowest<T>();
+    // entry bounds, lane-strided, in L's own pair order
+    T bt[JT];
+#pragma unroll
+    for (int j = 0; j < JT; j++)
+        bt[j] = (lane + 64 * j < NT) ? (T)0 : low;
+    if (P <= 8) {  // few pairs: a direct range loop
+#pragma unroll
+        for (int j = 0; j < JT; j++) {
+            const int t = lane + 64 * j;
+            if (t < NT) {
+                T b = 0;
+                for (int p = 0; p < P; p++) {
+                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                    const T *w = Wl + p * K;
+                    T m = w[lo];
+                    for (int k = lo + 1; k <= hi; k++)
+                        m = vmax<T>(m, w[k]);
+                    b += m;
+                }
+                bt[j] = b;
+            }
+        }
+    } else {
+        // many pairs: per pair the 8-wide running maxima M8[k] = max w[k..k+7]
+        // (clamped to K - 1); a range of width <= 16 is max(M8[lo],
+        // M8[max(lo, hi - 7)]) -- independent reads, not a dependent chain
+        for (int p = 0; p < P; p++) {
+            const T *w = Wl + p * K;
+            __builtin_amdgcn_wave_barrier();  // previous pair's M8 reads come first
+            for (int k = lane; k < K; k += 64) {
+                T m = w[k];
+#pragma unroll
+                for (int d = 1; d < 8; d++)
+                    m = vmax<T>(m, w[k + d < K ? k + d : K - 1]);
+                M8[k] = m;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < JT; j++) {
+                const int t = lane + 64 * j;
+                if (t < NT) {
+                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                    T m = M8[lo];
+                    for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
+                        m = vmax<T>(m, M8[k]);
+                    m = vmax<T>(m, M8[hi - 7 > lo ? hi - 7 : lo]);
+                    bt[j] += m;
+                }
+            }
+        }
+    }
+    // seed: the entry of largest bound (first on ties; NaN bounds never win)
+    T sv = low;
+    int st = 0;
+#pragma unroll
+    for (int j = 0; j < JT; j++)
+        if (bt[j] > sv) {
+            sv = bt[j];
+            st = lane + 64 * j;
+        }
+    for (int m = 32; m >= 1; m >>= 1)
+        better<T>(sv, st, (T)__shfl_xor(sv, m, 64), __shfl_xor(st, m, 64));
+    const int seed = __builtin_amdgcn_readfirstlane(st);
+
+    T best = low;
+    int bu = INT_MAX;
+    // evaluate one entry: one tuple per lane; only L > lowest is recorded (the
+    // exhaustive scan never records an L equal to its start value)
+    auto eval = [&](int t) {
+        const int start = tiles[2 * t], cnt = tiles[2 * t + 1];
+        T L = low;
+        int ui = INT_MAX;
+        if (lane < cnt) {
+            const int u = start + lane;
+            L = 0;
+#pragma unroll
+            for (int tw = 0; tw < TWC; tw++) {
+                if (tw < TW) {
+                    const uint32_t word = kp.bb_tuples[(size_t)u * TW + tw];
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const int p = 4 * tw + b;
+                        if (p < P)
+                            L += Wl[p * K + ((word >> (8 * b)) & 0xFFu)];
+                    }
+                }
+            }
+            ui = kp.bb_uidx[u];
+        }
+        const bool win = L > low && (L > best || (L == best && ui < bu));
+        if (__ballot(win) == 0)
+            return;
+        T v = win ? L : low;
+        int vi = win ? ui : INT_MAX;
+        for (int m = 32; m >= 1; m >>= 1)
+            better<T>(v, vi, (T)__shfl_xor(v, m, 64), __shfl_xor(vi, m, 64));
+        best = readlane(v, 0);
+        bu = __builtin_amdgcn_readfirstlane(vi);
+    };
+    if (NT > 0)
+        eval(seed);
+#pragma unroll
+    for (int j = 0; j < JT; j++) {
+        const int t = lane + 64 * j;
+        uint64_t mask = __ballot(t < NT && t != seed && !(bt[j] < best));
+        while (mask) {
+            const int l = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            if (!(readlane(bt[j], l) < best))  // the best may have risen since
+                eval(l + 64 * j);
+        }
+    }
+    best_out = best;
+    bu_out = bu;
+}
+
+}  // namespace tdoa_bb
