@@ -130,7 +130,13 @@ __device__ void stage_frames(const tdoa_kparams &kp, const Smem &sm, const int16
         if (ok) {
             r = c / cpr;
             const int k = c - r * cpr;
-            v = src[c];
+            if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
+                const int fl = r / kp.M, m = r - fl * kp.M;
+                v = reinterpret_cast<const uint4 *>(
+                    frames + ((int64_t)kp.frame_ids[f0 + fl] * kp.M + m) * kp.N)[k];
+            } else {
+                v = src[c];
+            }
             *reinterpret_cast<uint4 *>(&sm.X[r * RS + padw + 4 * k]) = v;
         }
         if (!PREPARED) {

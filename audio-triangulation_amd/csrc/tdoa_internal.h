@@ -55,6 +55,10 @@ struct tdoa_kparams {
     const uint16_t *bb_rng;    // [NT][P] lo | hi << 8
     const uint32_t *bb_tuples; // [U][TW] regrouped tuples
     const int32_t *bb_uidx;    // [U] their index in first-cell order
+    // DIRECT on the streaming batch: frame f of the batch is frames[frame_ids[f]]
+    // (the persistent trigger writes each frame at its stream's index); null:
+    // frame f is frames[f]
+    const int32_t *frame_ids;
     // least-squares refinement (tdoa_ls.hip)
     const float *mic_xy;       // [M][2] metres
     float fs, c, height;
@@ -123,6 +127,9 @@ int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
                    const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
                    int64_t B, void *stream);
 size_t tdoa_stream_trigger_lds(int M, int N, int H);
+// the trigger launch for this stream writes each triggered frame at its
+// stream's index (k_stream_trigger_p) instead of its compact slot
+bool tdoa_stream_trigger_by_id(const tdoa_stream_params &sp, int64_t S);
 int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream);
 int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &kp,
                               const tdoa_stream_kout &out, int64_t S, void *stream);

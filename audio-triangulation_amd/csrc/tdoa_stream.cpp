@@ -81,7 +81,9 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
     ko.lags = sp.fresh_lags;
     ko.gate = sp.fresh_gate;
     ko.weighted = sp.fresh;
-    rc = tdoa_launch_direct(st->kp, ko, sp.frames, st->S, false, s, nullptr, sp.count);
+    tdoa_kparams kp = st->kp;
+    kp.frame_ids = tdoa_stream_trigger_by_id(sp, st->S) ? sp.ids : nullptr;
+    rc = tdoa_launch_direct(kp, ko, sp.frames, st->S, false, s, nullptr, sp.count);
     if (rc)
         return rc;
     return tdoa_launch_stream_update(sp, st->kp, to_kout(out), st->S, s);

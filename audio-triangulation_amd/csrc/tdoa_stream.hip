@@ -365,17 +365,18 @@ __global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp,
 // cycles in SQ_WAIT_ANY).  A firing stream's frame is written from the words
 // the wave already holds, staged through LDS (no second read of the ring).
 template <int G, int M>
-__global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
+__global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
 {
     constexpr int H = 64 * G, N = 2 * H, CB = G * M, CW = CB / 4;
     static_assert(CB % 4 == 0, "a lane's chunk is whole words");
-    extern __shared__ __attribute__((aligned(16))) uint32_t stage_all[];  // [4 waves][3 H M / 4]
+    constexpr int NWB = 8;  // waves per workgroup
+    extern __shared__ __attribute__((aligned(16))) uint32_t stage_all[];  // [NWB waves][3 H M / 4]
+    __shared__ int nfired[NWB], slot_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t *stage = stage_all + wv * (3 * H * M / 4);
-    const int64_t GW = (int64_t)gridDim.x * 4;
-    int64_t s = (int64_t)blockIdx.x * 4 + wv;
-    if (s >= S)
-        return;  // whole wave: no workgroup barrier below
+    const int64_t GW = (int64_t)gridDim.x * NWB;
+    const int64_t s0 = (int64_t)blockIdx.x * NWB;  // the workgroup's first stream of an iteration
+    int64_t s = s0 + wv;
     const int64_t pos = *sp.pos;
     const int64_t base = pos + 1 - N;
     const int64_t cl = sp.capture_len;
@@ -409,12 +410,20 @@ __global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params 
         }
     };
     uint32_t wc[3][CW + 1], shc[3];
-    fetch(s, wc, shc);
-    int64_t rs = sp.ring_start[s];
+    int64_t rs = 0;
+    // this wave's triggered streams: lane i holds the i-th (stream, end)
+    int my_n = 0;
+    int my_id = 0;
+    int64_t my_end = 0;
+    if (s < S) {
+        fetch(s, wc, shc);
+        rs = sp.ring_start[s];
+    }
     constexpr int hb = __builtin_ctz(N) - 1;
     const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
-    for (;;) {
-        const uint8_t *cap = sp.capture + (size_t)s * cl * M;
+    for (int64_t sb = s0; sb < S; sb += GW, s += GW) {
+        const bool have = s < S;
+        const uint8_t *cap = sp.capture + (size_t)(have ? s : 0) * cl * M;
         uint32_t x[3][CW];
 #pragma unroll
         for (int r = 0; r < 3; r++) {
@@ -511,19 +520,18 @@ __global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params 
                 }
             }
         }
-        const uint64_t fire = __ballot(fi >= 0);
+        const uint64_t fire = have ? __ballot(fi >= 0) : 0;
         if (fire != 0) {
             const int fl = __builtin_ctzll(fire);  // lowest lane = lowest candidates
             const int a = G * fl + __builtin_amdgcn_readlane(fi, fl);
-            int slot = 0;
-            if (lane == 0) {
-                slot = atomicAdd(sp.count, 1);
-                const int64_t end = pos + 1 + a;
-                sp.ids[slot] = (int32_t)s;
-                sp.end[slot] = end;
-                sp.ring_start[s] = end;
+            const int64_t end = pos + 1 + a;
+            if (lane == my_n) {
+                my_id = (int)s;
+                my_end = end;
             }
-            slot = __builtin_amdgcn_readfirstlane(slot);
+            ++my_n;
+            if (lane == 0)
+                sp.ring_start[s] = end;
             // the frame (local samples a .. a + N - 1 of every mic, rolling_buffer.c:48-62
             // order) from the words in registers: rows 0..2 staged as [l][m] bytes
             __builtin_amdgcn_wave_barrier();  // the previous stream's stage reads come first
@@ -534,7 +542,10 @@ __global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params 
                     stage[r * (H * M / 4) + lane * CW + k] = x[r][k];
             __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
             const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
-            int16_t *dst = sp.frames + (size_t)slot * M * N;
+            // at the stream's own index: the compact list (ids, end) is
+            // written once per workgroup at the end (thousands of same-address
+            // slot atomics per hop serialise in L2: 53.5 vs 36.4 us)
+            int16_t *dst = sp.frames + (size_t)s * M * N;
 #pragma unroll 4
             for (int t = 0; t < N / 64; t++) {
                 const int n = lane + 64 * t;
@@ -543,10 +554,25 @@ __global__ void __launch_bounds__(256, 2) k_stream_trigger_p(tdoa_stream_params 
                     dst[(size_t)m * N + n] = (int16_t)sb[(a + n) * M + m];
             }
         }
-        if (sn >= S)
-            break;
-        s = sn;
         rs = rsn;
+    }
+    // the workgroup's triggered streams into the compact list: one atomic
+    if ((threadIdx.x & 63) == 0)
+        nfired[wv] = my_n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int n = 0;
+        for (int w = 0; w < NWB; w++)
+            n += nfired[w];
+        slot_base = n ? atomicAdd(sp.count, n) : 0;
+    }
+    __syncthreads();
+    int o = slot_base;
+    for (int w = 0; w < wv; w++)
+        o += nfired[w];
+    if (lane < my_n) {
+        sp.ids[o + lane] = my_id;
+        sp.end[o + lane] = my_end;
     }
 }
 
@@ -744,25 +770,41 @@ size_t tdoa_stream_trigger_lds(int M, int N, int H)
     return ((M * L * 2 + 15) & ~(size_t)15) + (((L + 1) * 4 + 15) & ~(size_t)15) + (L + 1) * 8;
 }
 
-template <int G, int M>
-static void launch_trigger_p(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
-{
-    const size_t lds = (size_t)4 * 3 * 64 * G * M;
-    const int res = tdoa_resident_blocks((const void *)k_stream_trigger_p<G, M>, 256, lds);
-    int64_t grid = (S + 3) / 4;
-    if (res > 0 && grid > res)
-        grid = res;
-    hipLaunchKernelGGL((k_stream_trigger_p<G, M>), dim3((unsigned)grid), dim3(256), lds, st, sp, S);
-}
-
-template <int G>
-static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+// the persistent register scan applies (and writes frames by stream id)
+static bool trigger_p_applies(const tdoa_stream_params &sp, int64_t S, int *res_out)
 {
     if (g_trigger_p < 0) {
         const char *e = getenv("TDOA_TRIGGER_P");
         g_trigger_p = e ? atoi(e) : 1;
     }
-    if (g_trigger_p) {
+    if (!g_trigger_p || !(sp.N == 2 * sp.H && ((uintptr_t)sp.capture & 3) == 0 &&
+                          sp.capture_len >= (int64_t)sp.N + 2 * sp.H))
+        return false;
+    if (!(sp.H == 256 || sp.H == 512 || sp.H == 1024) || sp.M < 2 || sp.M > 4)
+        return false;
+    (void)res_out;
+    return true;
+}
+
+template <int G, int M>
+static void launch_trigger_p(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+{
+    const size_t lds = (size_t)8 * 3 * 64 * G * M;
+    const int res = tdoa_resident_blocks((const void *)k_stream_trigger_p<G, M>, 512, lds);
+    int64_t grid = (S + 7) / 8;
+    if (res > 0 && grid > res)
+        grid = res;
+    // a wave lists at most 64 triggered streams (one per lane): <= 64 per wave
+    const int64_t min_grid = (S + 8 * 64 - 1) / (8 * 64);
+    if (grid < min_grid)
+        grid = min_grid;
+    hipLaunchKernelGGL((k_stream_trigger_p<G, M>), dim3((unsigned)grid), dim3(512), lds, st, sp, S);
+}
+
+template <int G>
+static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+{
+    if (trigger_p_applies(sp, S, nullptr)) {
         if (sp.M == 2)
             launch_trigger_p<G, 2>(sp, S, st);
         else if (sp.M == 3)
@@ -783,6 +825,11 @@ static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_
     else
         return false;
     return true;
+}
+
+bool tdoa_stream_trigger_by_id(const tdoa_stream_params &sp, int64_t S)
+{
+    return trigger_p_applies(sp, S, nullptr);
 }
 
 int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream)
