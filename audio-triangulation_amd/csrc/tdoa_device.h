@@ -12,6 +12,12 @@
 
 #include "tdoa_internal.h"
 
+#ifndef TDOA_GRID_MARK
+#define TDOA_GRID_MARK(i) \
+    do {                  \
+    } while (0)
+#endif
+
 namespace {
 
 
@@ -292,8 +298,10 @@ template <> __device__ __forceinline__ float lowest<float>() { return -INFINITY;
 
 template <typename T>
 __device__ void argmax_prior_phase(const tdoa_kparams &kp, T *scores, int *bestlag,
-                                   const tdoa_kout &out, int64_t f0, int nf)
+                                   const tdoa_kout &out, int64_t f0, int nf,
+                                   const float *prior_tab = nullptr)
 {
+    const float *prior = prior_tab ? prior_tab : kp.prior;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
     const int K = kp.K, P = kp.P;
     for (int fp = wave; fp < nf * P; fp += nwaves) {
@@ -318,13 +326,13 @@ __device__ void argmax_prior_phase(const tdoa_kparams &kp, T *scores, int *bestl
         const size_t gbase = (size_t)(f0 * P + fp) * K;
         if (k1 < K) {
             const int d = k1 > bk ? k1 - bk : bk - k1;
-            const T wv = apply_prior(v1, kp.prior[d]);
+            const T wv = apply_prior(v1, prior[d]);
             sc[k1] = wv;
             store_score(out, gbase + k1, v1, wv);
         }
         if (k2 < K) {
             const int d = k2 > bk ? k2 - bk : bk - k2;
-            const T wv = apply_prior(v2, kp.prior[d]);
+            const T wv = apply_prior(v2, prior[d]);
             sc[k2] = wv;
             store_score(out, gbase + k2, v2, wv);
         }
@@ -376,7 +384,7 @@ __device__ __forceinline__ void store_max(const tdoa_kout &o, int64_t i, float v
 template <typename T, int FMAX = TDOA_FMAX, int TWC = (TDOA_MAX_PAIRS + 3) / 4>
 __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, int *redi,
                              const tdoa_kout &out, int64_t f0, int nf,
-                             const uint32_t *tuples = nullptr)
+                             const uint32_t *tuples = nullptr, const int32_t *cells = nullptr)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
     const int nt = blockDim.x;
@@ -433,6 +441,7 @@ __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, i
                 }
         }
     }
+    TDOA_GRID_MARK(8);
 #pragma unroll
     for (int f = 0; f < FMAX; f++) {
         if (f < nf) {
@@ -445,6 +454,7 @@ __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, i
         }
     }
     __syncthreads();
+    TDOA_GRID_MARK(9);
     if (tid < nf) {
         const int f = tid;
         T v = redv[f];
@@ -453,7 +463,7 @@ __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, i
             better(v, ui, redv[w * FMAX + f], redi[w * FMAX + f]);
         if (ui < 0 || ui >= U)  // only if every L compared false (NaN scores)
             ui = 0;
-        const int cell = kp.tuple_cell[ui];
+        const int cell = cells ? cells[ui] : kp.tuple_cell[ui];
         const int64_t fi = f0 + f;
         if (out.cell)
             out.cell[fi] = cell;

@@ -25,13 +25,12 @@
 #include <cstdlib>
 
 #include "tdoa_internal.h"
-#include "tdoa_device.h"
 
 int tdoa_set_error(int code, const char *msg);
 
 #ifdef TDOA_DIAG
 // Diagnostic build only (libtdoa_diag.so): per-workgroup phase stamps.
-#define TDOA_DIAG_SLOTS 8
+#define TDOA_DIAG_SLOTS 16
 __device__ unsigned long long g_diag[1 << 20];
 #define DIAG_STAMP(i)                                                   \
     do {                                                                \
@@ -39,11 +38,14 @@ __device__ unsigned long long g_diag[1 << 20];
             g_diag[(size_t)blockIdx.x * TDOA_DIAG_SLOTS + (i)] =        \
                 __builtin_amdgcn_s_memtime();                           \
     } while (0)
+#define TDOA_GRID_MARK(i) DIAG_STAMP(i)
 #else
 #define DIAG_STAMP(i) \
     do {              \
     } while (0)
 #endif
+
+#include "tdoa_device.h"
 
 namespace {
 
@@ -101,11 +103,314 @@ __device__ __forceinline__ v4i_mf mf_limbs(const uint32_t (&w)[8], uint32_t sel)
     return r;
 }
 
-template <bool PREPARED, int TWC>
+// ---- DPP wave reductions (no LDS round trips): the butterfly of
+// tdoa_fft32.h -- xor 1, xor 2, half-row mirror, row mirror, then
+// row_bcast:15 into rows 1, 3 and row_bcast:31 into rows 2, 3 -- leaves the
+// result in lane 63 (and, without the last step, each half-wave's in lanes 31 / 63)
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void dpp_sum_step(int &x)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, CTRL, RM, 0xF, false);
+}
+// sum over each aligned group of `width` lanes (4 .. 64, uniform): the group's
+// last lane holds it (every lane of the group for width <= 16)
+__device__ __forceinline__ int group_sum_dpp(int x, int width)
+{
+    dpp_sum_step<0xB1, 0xF>(x);
+    dpp_sum_step<0x4E, 0xF>(x);
+    if (width > 4)
+        dpp_sum_step<0x141, 0xF>(x);
+    if (width > 8)
+        dpp_sum_step<0x140, 0xF>(x);
+    if (width > 16)
+        dpp_sum_step<0x142, 0xA>(x);
+    if (width > 32)
+        dpp_sum_step<0x143, 0xC>(x);
+    return x;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void dpp_umax_step(uint64_t &k)
+{
+    const uint32_t lo = (uint32_t)dpp_i<CTRL, RM>((int)(uint32_t)k);
+    const uint32_t hi = (uint32_t)dpp_i<CTRL, RM>((int)(uint32_t)(k >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    k = o > k ? o : k;
+}
+// unsigned 64-bit max of the wave -> lane 63
+__device__ __forceinline__ uint64_t wave_umax_dpp(uint64_t k)
+{
+    dpp_umax_step<0xB1, 0xF>(k);
+    dpp_umax_step<0x4E, 0xF>(k);
+    dpp_umax_step<0x141, 0xF>(k);
+    dpp_umax_step<0x140, 0xF>(k);
+    dpp_umax_step<0x142, 0xA>(k);
+    dpp_umax_step<0x143, 0xC>(k);
+    return k;
+}
+__device__ __forceinline__ uint64_t lane63_u64(uint64_t k)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Exact int64 (value, first index) maxima as one unsigned key: |score| <=
+// N * 2^30 <= 2^42 (N <= 4096) and |L| <= 28 * 2^42 < 2^47, so
+// key = (v + 2^47) << IB | (2^IB - 1 - index) orders by value, then by the
+// smaller index, in 48 + IB <= 62 bits.  Argmax: index = lag slot (IB = 7,
+// correlations.c:20-23 keeps the first maximum); grid: index = the tuple's
+// first cell (IB = 14) -- tuple order is first-cell order, so the smallest
+// cell among equal L is the first row-major argmax of vga_heatmap.h:99-108.
+constexpr int64_t KEY_BIAS = (int64_t)1 << 47;
+template <int IB>
+__device__ __forceinline__ uint64_t vkey(int64_t v, int idx)
+{
+    return ((uint64_t)(v + KEY_BIAS) << IB) | (uint64_t)((1 << IB) - 1 - idx);
+}
+template <int IB>
+__device__ __forceinline__ int64_t key_value(uint64_t k)
+{
+    return (int64_t)(k >> IB) - KEY_BIAS;
+}
+template <int IB>
+__device__ __forceinline__ int key_index(uint64_t k)
+{
+    return (1 << IB) - 1 - (int)(k & ((1u << IB) - 1));
+}
+
+// argmax + lag prior + gate (correlations.c:20-33, sample_compute.h:124-134)
+// for the matrix-core kernel: one wave per (frame, pair), DPP key reduction
+__device__ void argmax_prior_mf(const tdoa_kparams &kp, int64_t *scores, int *bestlag, const float *prior,
+                                const tdoa_kout &out, int64_t f0, int nf)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const int K = kp.K, P = kp.P;
+    for (int fp = wave; fp < nf * P; fp += nwaves) {
+        int64_t *sc = scores + fp * K;
+        const int k1 = lane, k2 = lane + 64;
+        const int64_t v1 = k1 < K ? sc[k1] : 0, v2 = k2 < K ? sc[k2] : 0;
+        uint64_t key = k1 < K ? vkey<7>(v1, k1) : 0;
+        if (k2 < K) {
+            const uint64_t k2k = vkey<7>(v2, k2);
+            key = k2k > key ? k2k : key;
+        }
+        const int bk = key_index<7>(lane63_u64(wave_umax_dpp(key)));
+        const size_t gbase = (size_t)(f0 * P + fp) * K;
+        if (k1 < K) {
+            const int d = k1 > bk ? k1 - bk : bk - k1;
+            const int64_t wv = apply_prior(v1, prior[d]);
+            sc[k1] = wv;
+            store_score(out, gbase + k1, v1, wv);
+        }
+        if (k2 < K) {
+            const int d = k2 > bk ? k2 - bk : bk - k2;
+            const int64_t wv = apply_prior(v2, prior[d]);
+            sc[k2] = wv;
+            store_score(out, gbase + k2, v2, wv);
+        }
+        if (lane == 0) {
+            bestlag[fp] = bk - kp.S;
+            out.lags[f0 * P + fp] = bk - kp.S;
+        }
+    }
+    __syncthreads();
+    if (out.gate) {
+        for (int f = tid; f < nf; f += blockDim.x) {
+            int tot = 0;
+            for (int p = 0; p < P; p++) {
+                const int b = bestlag[f * P + p];
+                tot += b * b;
+            }
+            out.gate[f0 + f] = tot > 4 ? 1 : 0;
+        }
+    }
+}
+
+// grid solve (vga_heatmap.h:99-108) of the workgroup's <= 4 frames for
+// single-word tuples: the thread's <= GR tuple words and first cells were
+// loaded at the kernel's start (q, cl); per frame the key maximum over the
+// thread's tuples, the wave (DPP) and the workgroup (LDS, one barrier)
+template <int GR>
+__device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t *red, const uint32_t (&q)[GR],
+                        const int32_t (&cl)[GR], const tdoa_kout &out, int64_t f0, int nf)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6, nt = blockDim.x;
+    const int K = kp.K, P = kp.P, U = kp.U;
+    uint64_t best[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < GR; r++) {
+        if (tid + r * nt < U) {
+            int64_t L[4] = {0, 0, 0, 0};
+            for (int p = 0; p < P; p++) {
+                const int idx = p * K + ((q[r] >> (8 * p)) & 0xFFu);
+#pragma unroll
+                for (int f = 0; f < 4; f++)
+                    if (f < nf)
+                        L[f] += scores[f * P * K + idx];
+            }
+#pragma unroll
+            for (int f = 0; f < 4; f++) {
+                const uint64_t k = vkey<14>(L[f], cl[r]);
+                best[f] = k > best[f] ? k : best[f];
+            }
+        }
+    }
+    TDOA_GRID_MARK(8);
+#pragma unroll
+    for (int f = 0; f < 4; f++)
+        best[f] = wave_umax_dpp(best[f]);
+    if (lane == 63)
+#pragma unroll
+        for (int f = 0; f < 4; f++)
+            red[wave * 4 + f] = best[f];
+    __syncthreads();
+    TDOA_GRID_MARK(9);
+    if (tid < nf) {
+        const int f = tid;
+        uint64_t k = red[f];
+        for (int w = 1; w < nwaves; w++) {
+            const uint64_t o = red[w * 4 + f];
+            k = o > k ? o : k;
+        }
+        const int cell = key_index<14>(k);
+        const int64_t fi = f0 + f;
+        if (out.cell)
+            out.cell[fi] = cell;
+        if (out.max_L)
+            out.max_L[fi] = key_value<14>(k);
+        if (out.xy) {
+            const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+            out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
+            out.xy[2 * fi + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+        }
+    }
+}
+
+// LDS side tables of k_direct_mfma beyond Smem (byte offsets, host-computed):
+// rsum [F*M][4] the prepared rows' sums (whole row, first 16 / 32 / 48
+// samples); prior [K] the lag prior; red [16][4] u64 grid keys per wave
+struct MfTabs {
+    int rsum, prior, red;
+};
+
+// Frames -> LDS in the offset-byte form the matrix cores read (x ^ 0x0080 per
+// sample: high byte and low byte - 128 both int8), fused into one pass per
+// chunk (16 B = 8 samples):
+//   every global read of the phase (frame chunks, window chunks, the prior,
+//   grid tables) is issued first -- one HBM latency, not one per pass;
+//   the raw row sums (rolling_buffer.c:48-62 floor mean) by wave sums + one LDS
+//   atomic per wave and row; then, from the chunks still in registers, the
+//   prep (rolling_buffer.c:64-66, buffer.c:13-16, buffer.c:4-11), the prepared
+//   rows' sums for the offset correction, and the offset form, stored once.
+// CH: chunks per thread (>= ceil(F*M*N/8 / threads), host-checked).
+template <bool PREPARED, int CH>
+__device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm, char *smem, const MfTabs &tb,
+                                         const int16_t *__restrict__ frames, int64_t f0, int nf)
+{
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int rows = nf * kp.M, NW = kp.N / 2, padw = kp.PADW, RS = kp.RS;
+    int *rsum = reinterpret_cast<int *>(smem + tb.rsum);
+    const int cpr = kp.N / 8;  // 16-byte chunks per row
+    const int nchunk = rows * cpr;
+    const int width = cpr < 64 ? cpr : 64;  // lanes of one wave that share a row
+    uint4 v[CH], w[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+        const int c = tid + nt * i;
+        v[i] = make_uint4(0, 0, 0, 0);
+        w[i] = make_uint4(0, 0, 0, 0);
+        if (c < nchunk) {
+            const int r = c / cpr, k = c - r * cpr;
+            if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
+                const int fl = r / kp.M, m = r - fl * kp.M;
+                v[i] = reinterpret_cast<const uint4 *>(frames + ((int64_t)kp.frame_ids[f0 + fl] * kp.M + m) * kp.N)[k];
+            } else {
+                v[i] = reinterpret_cast<const uint4 *>(frames + f0 * kp.M * kp.N)[c];
+            }
+            if (!PREPARED)
+                w[i] = reinterpret_cast<const uint4 *>(kp.window)[k];
+        }
+    }
+    // the prior: requested now, written once the frames have arrived
+    const float pr = tid < kp.K ? kp.prior[tid] : 0.0f;
+    // pads are zero samples (offset form 0x0080 per sample); sums start at 0
+    for (int i = tid; i < rows * 2 * padw; i += nt) {
+        const int r = i / (2 * padw), k = i - r * 2 * padw;
+        sm.X[r * RS + (k < padw ? k : NW + k)] = 0x00800080u;
+    }
+    for (int i = tid; i < rows; i += nt)
+        sm.sums[i] = 0;
+    for (int i = tid; i < 4 * rows; i += nt)
+        rsum[i] = 0;
+    __syncthreads();  // sums zeroed
+    DIAG_STAMP(6);
+    // lane `width - 1` of each group of lanes sharing a row adds its group's sum
+    auto wsum = [&](int x) { return group_sum_dpp(x, width); };
+    const bool adder = (tid & (width - 1)) == width - 1;
+    if (!PREPARED) {
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            const int c = tid + nt * i;
+            if (nt * i < nchunk) {  // uniform: the wave's lanes join the shuffles
+                const int s = wsum(sum_word(v[i].x) + sum_word(v[i].y) + sum_word(v[i].z) + sum_word(v[i].w));
+                if (c < nchunk && adder)
+                    atomicAdd(&sm.sums[c / cpr], s);
+            }
+        }
+        __syncthreads();  // row sums complete
+    }
+    DIAG_STAMP(7);
+    if (tid < kp.K)
+        reinterpret_cast<float *>(smem + tb.prior)[tid] = pr;
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+        const int c = tid + nt * i;
+        if (nt * i < nchunk) {
+            const bool ok = c < nchunk;
+            const int r = ok ? c / cpr : 0, k = c - r * cpr;
+            uint4 x = v[i];
+            if (!PREPARED) {
+                // floor mean: int64 `total >> BITS` == int32 arithmetic shift here
+                const uint32_t off16 = (uint32_t)(sm.sums[r] >> kp.log2N) & 0xFFFFu;
+                x.x = prep_word(x.x, off16, w[i].x);
+                x.y = prep_word(x.y, off16, w[i].y);
+                x.z = prep_word(x.z, off16, w[i].z);
+                x.w = prep_word(x.w, off16, w[i].w);
+            }
+            const int ps = ok ? sum_word(x.x) + sum_word(x.y) + sum_word(x.z) + sum_word(x.w) : 0;
+            const int s = wsum(ps);
+            if (ok) {
+                if (adder)
+                    atomicAdd(&rsum[4 * r], s);
+                // first 16 / 32 / 48 samples: chunks 0-1 / 0-3 / 0-5 of the row
+                if (k < 6) {
+                    if (k < 2)
+                        atomicAdd(&rsum[4 * r + 1], ps);
+                    if (k < 4)
+                        atomicAdd(&rsum[4 * r + 2], ps);
+                    atomicAdd(&rsum[4 * r + 3], ps);
+                }
+                x.x ^= 0x00800080u;
+                x.y ^= 0x00800080u;
+                x.z ^= 0x00800080u;
+                x.w ^= 0x00800080u;
+                *reinterpret_cast<uint4 *>(&sm.X[r * RS + padw + 4 * k]) = x;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <bool PREPARED, int TWC, int CH>
 __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
                                                       const int16_t *__restrict__ frames, int64_t B,
                                                       const int32_t *__restrict__ count, int n0, int nq,
-                                                      int rsum_off)
+                                                      MfTabs tb)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
@@ -117,36 +422,28 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
             return;
     }
     const int nf = (int)((B - f0) < kp.F ? (B - f0) : kp.F);
-    stage_frames<PREPARED>(kp, sm, frames, f0, nf);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-    const int RS = kp.RS, rows = nf * kp.M, words = rows * RS;
-    // per row: sum of the row and of its first 16 / 32 / 48 samples (one wave a row)
-    int *rsum = reinterpret_cast<int *>(smem + rsum_off);
-    for (int row = wave; row < rows; row += nwaves) {
-        const uint32_t *x = sm.X + row * RS + kp.PADW;
-        const int v0 = sum_word(x[lane]);
-        int t = v0;
-        for (int i = lane + 64; i < kp.N / 2; i += 64)
-            t += sum_word(x[i]);
-        int p16 = lane < 8 ? v0 : 0, p32 = lane < 16 ? v0 : 0, p48 = lane < 24 ? v0 : 0;
+    DIAG_STAMP(0);
+    // single-word tuples (P <= 4): this thread's grid tuples and their first
+    // cells, requested now and consumed by the grid solve at the end
+    constexpr int GR = 4;
+    constexpr bool KEYGRID = TWC == 1;
+    uint32_t gq[GR];
+    int32_t gc[GR];
+    const bool do_grid = out.cell || out.xy || out.max_L;
+    if constexpr (KEYGRID) {
 #pragma unroll
-        for (int m = 1; m < 64; m <<= 1) {
-            t += __shfl_xor(t, m, 64);
-            p16 += __shfl_xor(p16, m, 64);
-            p32 += __shfl_xor(p32, m, 64);
-            p48 += __shfl_xor(p48, m, 64);
-        }
-        if (lane == 0) {
-            rsum[4 * row + 0] = t;
-            rsum[4 * row + 1] = p16;
-            rsum[4 * row + 2] = p32;
-            rsum[4 * row + 3] = p48;
+        for (int r = 0; r < GR; r++) {
+            const int u = (int)threadIdx.x + r * (int)blockDim.x;
+            gq[r] = do_grid && u < kp.U ? kp.tuples[u] : 0u;
+            gc[r] = do_grid && u < kp.U ? kp.tuple_cell[u] : 0;
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < words; i += blockDim.x)
-        sm.X[i] ^= 0x00800080u;
-    __syncthreads();
+    stage_mf<PREPARED, CH>(kp, sm, smem, tb, frames, f0, nf);
+    DIAG_STAMP(1);
+    DIAG_STAMP(2);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const int *rsum = reinterpret_cast<const int *>(smem + tb.rsum);
+    const int RS = kp.RS;
 
     const int g = lane >> 4, r = lane & 15, rr = r < nq ? r : nq - 1;
     const int K = kp.K, S = kp.S, P = kp.P, NB = kp.N / 64 + 1;
@@ -195,11 +492,18 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
         }
     }
     __syncthreads();
-    argmax_prior_phase<int64_t>(kp, sm.scores, sm.best, out, f0, nf);
+    DIAG_STAMP(3);
+    argmax_prior_mf(kp, sm.scores, sm.best, reinterpret_cast<const float *>(smem + tb.prior), out, f0, nf);
+    DIAG_STAMP(4);
     // grid solve (vga_heatmap.h:99-108) on the weighted scores still in LDS:
     // no [B][P][K] round trip through HBM and no second launch
-    if (out.cell || out.xy || out.max_L)
-        grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf);
+    if (do_grid) {
+        if constexpr (KEYGRID)
+            grid_mf<GR>(kp, sm.scores, reinterpret_cast<uint64_t *>(smem + tb.red), gq, gc, out, f0, nf);
+        else
+            grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf);
+    }
+    DIAG_STAMP(5);
 }
 
 // --------------------------------------------------------------- EMA
@@ -415,8 +719,18 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         kp.RS = kp.N / 2 + 2 * MF_PADW;
         kp.F = kp.P >= 16 ? 1 : 16 / kp.P > 4 ? 4 : 16 / kp.P;  // frames per workgroup: one wave per (frame, pair) up to 16
         threads = 64 * (kp.F * kp.P < 16 ? kp.F * kp.P : 16);
-        const size_t rsum_off = smem_bytes(kp, threads / 64);
-        const size_t lds = rsum_off + (size_t)16 * kp.F * kp.M;
+        MfTabs tb;
+        size_t o = smem_bytes(kp, threads / 64);
+        tb.rsum = (int)o;
+        o += (size_t)16 * kp.F * kp.M;
+        tb.prior = (int)o;
+        o += (size_t)128 * 4;
+        tb.red = (int)o;
+        o += (size_t)16 * 4 * 8;
+        // single-word tuples: each thread holds <= 4 of the grid's tuples
+        if (kp.TW == 1 && kp.U > 4 * threads)
+            return tdoa_set_error(-1, "DIRECT: more distinct lag tuples than the grid solve holds");
+        const size_t lds = (o + 15) & ~(size_t)15;
         if (lds > 160 * 1024)
             return tdoa_set_error(-1, "DIRECT: shape needs more than 160 KiB LDS per workgroup");
         if (lds_bytes_out)
@@ -424,22 +738,35 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         const int64_t grid = (B + kp.F - 1) / kp.F;
         if (grid > INT_MAX)
             return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
+        const int chunks = (kp.F * kp.M * kp.N / 8 + threads - 1) / threads;  // per thread
+        if (chunks > 8)
+            return tdoa_set_error(-1, "DIRECT: frames too large for the staging registers");
         hipStream_t st = (hipStream_t)stream;
         constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
-#define TDOA_LAUNCH_MF(PREP, TWC)                                                                 \
-    hipLaunchKernelGGL((k_direct_mfma<PREP, TWC>), dim3((unsigned)grid), dim3(threads), lds, st, kp, \
-                       out, frames, B, count_dev, n0, nq, (int)rsum_off)
+#define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                  \
+    hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH>), dim3((unsigned)grid), dim3(threads), lds, st, kp, \
+                       out, frames, B, count_dev, n0, nq, tb)
+#define TDOA_LAUNCH_MF_CH(PREP, TWC)      \
+    do {                                  \
+        if (chunks <= 2)                  \
+            TDOA_LAUNCH_MF(PREP, TWC, 2); \
+        else if (chunks <= 4)             \
+            TDOA_LAUNCH_MF(PREP, TWC, 4); \
+        else                              \
+            TDOA_LAUNCH_MF(PREP, TWC, 8); \
+    } while (0)
         if (kp.TW == 1) {
             if (prepared)
-                TDOA_LAUNCH_MF(true, 1);
+                TDOA_LAUNCH_MF_CH(true, 1);
             else
-                TDOA_LAUNCH_MF(false, 1);
+                TDOA_LAUNCH_MF_CH(false, 1);
         } else {
             if (prepared)
-                TDOA_LAUNCH_MF(true, TWX);
+                TDOA_LAUNCH_MF_CH(true, TWX);
             else
-                TDOA_LAUNCH_MF(false, TWX);
+                TDOA_LAUNCH_MF_CH(false, TWX);
         }
+#undef TDOA_LAUNCH_MF_CH
 #undef TDOA_LAUNCH_MF
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : hip_fail(e, "k_direct_mfma launch");

@@ -63,12 +63,14 @@ CONFIGS = {
 
 
 def dominant_kernel(config: int, engine: str) -> str:
-    """Name of the kernel a config-2 launch runs (the one `traffic` was measured on)."""
+    """Name of the kernel(s) a launch runs (the ones `traffic` was measured on)."""
     if config == 2 and engine == "gcc_phat":
         w = os.environ.get("TDOA_PHAT1024_WAVES", "8")
         return {"8": "k_p1k_lean", "4": "k_phat1024"}.get(w, "k_gcc_phat_1024")
     if config == 2:
         return "k_direct_mfma" if os.environ.get("TDOA_DIRECT_MFMA", "1") != "0" else "k_direct"
+    if config in (3, 4) and engine == "gcc_phat" and os.environ.get("TDOA_PHAT_FUSED", "1") != "0":
+        return "k_frame16 + k_grid_bb"
     return ""
 
 
@@ -354,11 +356,19 @@ def traffic_entry(args):
     except (OSError, ValueError):
         return None, None
     e = tj.get(f"c{args.config}_{args.engine}") or {}
-    if e.get("kernel") != kname:
+    names = kname.split(" + ")
+    if e.get("kernel") != names[0]:
         return None, None
     src = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
            f"passes on {kname} ({e.get('date', 'undated')}), read = 2 x FETCH_SIZE")
-    return e.get("hbm_bytes_per_launch"), src
+    if len(names) == 1:
+        return e.get("hbm_bytes_per_launch"), src
+    # several kernels per launch: the sum of theirs (each dispatched once per launch)
+    ks = e.get("kernels", {})
+    per = [sum(v["hbm_bytes"] for k, v in ks.items() if k.startswith(n + "<") or k == n) for n in names]
+    if not all(per):
+        return None, None
+    return sum(per), src
 
 
 def main():
@@ -453,7 +463,17 @@ def main_stream(args, dev, ri, cache):
             "stream": {k: res[k] for k in ("kernel_ms", "triggered", "gated",
                                            "stream_samples_per_s", "realtime_streams")},
             "latency_ms": res["latency_ms"],
-            "roofline": None,
+            # the hop's algorithmic bytes: every stream's 512 capture samples (M bytes
+            # each) read once, over the hop's GPU time (memset + trigger + DIRECT +
+            # update, HIP events on the pipeline stream)
+            "roofline": {"bound": "hbm", "achieved": res["capture_bytes_per_step"] / ri.world /
+                         (res["kernel_ms"] * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": res["capture_bytes_per_step"] / ri.world / (res["kernel_ms"] * 1e-3) / 1e9
+                         / HBM_PEAK_GBS,
+                         "traffic": None, "traffic_source": None,
+                         "kernel": "all kernels of a hop (hipGraph)", "kernel_ms": res["kernel_ms"],
+                         "bytes_per_step": res["capture_bytes_per_step"] // ri.world},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu:

@@ -202,19 +202,26 @@ def _grid_f32(weighted, lut):
     return L.argmax(-1).astype(np.int32), L.max(-1)
 
 
-@pytest.mark.parametrize("kind", ["adc", "adc_3iter", "adc_ragged", "full_range", "noise_only"])
+@pytest.mark.parametrize("kind", ["adc", "adc_3iter", "adc_ragged", "full_range", "noise_only",
+                                  "constant", "mixed"])
 def test_grid_exact_on_own_scores(phat3, kind):
-    """The config-2 kernel scans the 2469 distinct lag tuples once per two
-    iterations for a wave's four frames; its cell and max L must equal the
-    exhaustive float32 scan of its own weighted scores bit for bit (ties to the
-    first row-major cell).  6144 frames give every wave three iterations (one
-    paired grid pass, one single); 6151 leave a ragged last workgroup."""
+    """The config-2 kernel scans the 2469 distinct lag tuples for a wave's two
+    frames at once; its cell and max L must equal the exhaustive float32 scan
+    of its own weighted scores bit for bit (ties to the first row-major cell):
+    peaked, flat noisy and all-equal scores (every tuple ties), and waves whose
+    two frames are one peaked and one constant.  6144 / 6151 frames: several
+    workgroups per CU, a ragged last workgroup."""
     lut = phat3.lut()
     if kind.startswith("adc"):
         B = {"adc": 2048, "adc_3iter": 6144, "adc_ragged": 6151}[kind]
         fr, _, _ = synth.adc_frames(B, 3, 1024, lut.reshape(3, 101, 101), 46, 77, device="cuda")
     elif kind == "full_range":
         fr = synth.full_range_frames(512, 3, 1024, 0x51, device="cuda")
+    elif kind == "constant":
+        fr = torch.full((64, 3, 1024), 77, dtype=torch.int16, device="cuda")
+    elif kind == "mixed":  # frames 2w peaked, 2w + 1 constant: one wave, both extremes
+        fr, _, _ = synth.adc_frames(256, 3, 1024, lut.reshape(3, 101, 101), 46, 78, device="cuda")
+        fr[1::2] = 77
     else:  # uncorrelated mics: flat, noisy scores, weak bounds
         g = torch.Generator(device="cpu").manual_seed(5)
         fr = (torch.randint(0, 256, (512, 3, 1024), generator=g, dtype=torch.int16)).cuda()

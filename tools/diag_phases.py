@@ -31,21 +31,35 @@ def main():
     torch.cuda.synchronize()
     L = tdoa.load()
     L.tdoa_diag_fetch.argtypes = [C.c_void_p, C.c_int]
-    n = 8 * 4096
+    n = 16 * 4096
     buf = np.zeros(n, np.uint64)
     assert L.tdoa_diag_fetch(buf.ctypes.data_as(C.c_void_p), n) == 0
-    st = buf.reshape(-1, 8).astype(np.int64)
+    st = buf.reshape(-1, 16 if os.environ.get('TDOA_DIRECT_MFMA', '1') != '0' else 8).astype(np.int64)
     nwg = int((st[:, 0] != 0).sum())
     st = st[:nwg]
-    names = ["stage", "xcorr", "argmax+prior", "grid"]
-    d = np.diff(st[:, :5], axis=1)
-    tot = st[:, 4] - st[:, 0]
+    mfma = os.environ.get("TDOA_DIRECT_MFMA", "1") != "0"
+    names = (["stage", "sums+xor", "xcorr", "argmax+prior", "grid"] if mfma else
+             ["stage", "xcorr", "argmax+prior", "grid"])
+    ns = len(names)
+    d = np.diff(st[:, :ns + 1], axis=1)
+    tot = st[:, ns] - st[:, 0]
     print(f"engine={engine} B={B} workgroups={nwg}")
     for i, nm in enumerate(names):
         print(f"  {nm:14s} median {np.median(d[:, i]):9.0f} cyc  ({np.median(d[:, i]) / np.median(tot) * 100:5.1f}%)")
     print(f"  total          median {np.median(tot):9.0f} cyc")
-    span = st[:, 4].max() - st[:, 0].min()
+    if mfma:
+        print("  stage split: tables+pads %d, raw sums %d, prep+store %d cyc (median)" %
+              (np.median(st[:, 6] - st[:, 0]), np.median(st[:, 7] - st[:, 6]), np.median(st[:, 1] - st[:, 7])))
+        print("  grid split: scan %d, wave reductions + barrier %d, final %d cyc (median)" %
+              (np.median(st[:, 8] - st[:, 4]), np.median(st[:, 9] - st[:, 8]), np.median(st[:, 5] - st[:, 9])))
+    span = st[:, ns].max() - st[:, 0].min()
     print(f"  launch span {span} cyc")
+    t0 = st[:, 0] - st[:, 0].min()
+    print("  workgroup start (cyc from first): p25 %d p50 %d p75 %d p90 %d max %d" %
+          tuple(np.percentile(t0, [25, 50, 75, 90, 100])))
+    te = st[:, ns] - st[:, 0].min()
+    print("  workgroup end:                    p25 %d p50 %d p75 %d p90 %d max %d" %
+          tuple(np.percentile(te, [25, 50, 75, 90, 100])))
 
 
 if __name__ == "__main__":
