@@ -46,6 +46,7 @@ __device__ unsigned long long g_diag[1 << 20];
 #endif
 
 #include "tdoa_device.h"
+#include "tdoa_keys.h"
 
 namespace {
 
@@ -103,97 +104,29 @@ __device__ __forceinline__ v4i_mf mf_limbs(const uint32_t (&w)[8], uint32_t sel)
     return r;
 }
 
-// ---- DPP wave reductions (no LDS round trips): the butterfly of
-// tdoa_fft32.h -- xor 1, xor 2, half-row mirror, row mirror, then
-// row_bcast:15 into rows 1, 3 and row_bcast:31 into rows 2, 3 -- leaves the
-// result in lane 63 (and, without the last step, each half-wave's in lanes 31 / 63)
-template <int CTRL, int RM>
-__device__ __forceinline__ int dpp_i(int v)
+// LDS score table of the matrix-core kernel: [F][P][K], or for single-word
+// tuples (F = 4) frame-interleaved [P][K][4] -- the grid solve then reads a
+// slot's four frames with two 16-B reads instead of four 8-B reads
+template <bool IL>
+__device__ __forceinline__ int sidx(int f, int p, int k, int P, int K)
 {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xF, false);
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ void dpp_sum_step(int &x)
-{
-    x += __builtin_amdgcn_update_dpp(0, x, CTRL, RM, 0xF, false);
-}
-// sum over each aligned group of `width` lanes (4 .. 64, uniform): the group's
-// last lane holds it (every lane of the group for width <= 16)
-__device__ __forceinline__ int group_sum_dpp(int x, int width)
-{
-    dpp_sum_step<0xB1, 0xF>(x);
-    dpp_sum_step<0x4E, 0xF>(x);
-    if (width > 4)
-        dpp_sum_step<0x141, 0xF>(x);
-    if (width > 8)
-        dpp_sum_step<0x140, 0xF>(x);
-    if (width > 16)
-        dpp_sum_step<0x142, 0xA>(x);
-    if (width > 32)
-        dpp_sum_step<0x143, 0xC>(x);
-    return x;
-}
-template <int CTRL, int RM>
-__device__ __forceinline__ void dpp_umax_step(uint64_t &k)
-{
-    const uint32_t lo = (uint32_t)dpp_i<CTRL, RM>((int)(uint32_t)k);
-    const uint32_t hi = (uint32_t)dpp_i<CTRL, RM>((int)(uint32_t)(k >> 32));
-    const uint64_t o = ((uint64_t)hi << 32) | lo;
-    k = o > k ? o : k;
-}
-// unsigned 64-bit max of the wave -> lane 63
-__device__ __forceinline__ uint64_t wave_umax_dpp(uint64_t k)
-{
-    dpp_umax_step<0xB1, 0xF>(k);
-    dpp_umax_step<0x4E, 0xF>(k);
-    dpp_umax_step<0x141, 0xF>(k);
-    dpp_umax_step<0x140, 0xF>(k);
-    dpp_umax_step<0x142, 0xA>(k);
-    dpp_umax_step<0x143, 0xC>(k);
-    return k;
-}
-__device__ __forceinline__ uint64_t lane63_u64(uint64_t k)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 63);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), 63);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// Exact int64 (value, first index) maxima as one unsigned key: |score| <=
-// N * 2^30 <= 2^42 (N <= 4096) and |L| <= 28 * 2^42 < 2^47, so
-// key = (v + 2^47) << IB | (2^IB - 1 - index) orders by value, then by the
-// smaller index, in 48 + IB <= 62 bits.  Argmax: index = lag slot (IB = 7,
-// correlations.c:20-23 keeps the first maximum); grid: index = the tuple's
-// first cell (IB = 14) -- tuple order is first-cell order, so the smallest
-// cell among equal L is the first row-major argmax of vga_heatmap.h:99-108.
-constexpr int64_t KEY_BIAS = (int64_t)1 << 47;
-template <int IB>
-__device__ __forceinline__ uint64_t vkey(int64_t v, int idx)
-{
-    return ((uint64_t)(v + KEY_BIAS) << IB) | (uint64_t)((1 << IB) - 1 - idx);
-}
-template <int IB>
-__device__ __forceinline__ int64_t key_value(uint64_t k)
-{
-    return (int64_t)(k >> IB) - KEY_BIAS;
-}
-template <int IB>
-__device__ __forceinline__ int key_index(uint64_t k)
-{
-    return (1 << IB) - 1 - (int)(k & ((1u << IB) - 1));
+    return IL ? ((p * K + k) << 2) + f : (f * P + p) * K + k;
 }
 
 // argmax + lag prior + gate (correlations.c:20-33, sample_compute.h:124-134)
 // for the matrix-core kernel: one wave per (frame, pair), DPP key reduction
+template <bool IL>
 __device__ void argmax_prior_mf(const tdoa_kparams &kp, int64_t *scores, int *bestlag, const float *prior,
                                 const tdoa_kout &out, int64_t f0, int nf)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
     const int K = kp.K, P = kp.P;
     for (int fp = wave; fp < nf * P; fp += nwaves) {
-        int64_t *sc = scores + fp * K;
+        const int ff = fp / P, pp = fp - ff * P;
+        int64_t *sc = scores + sidx<IL>(ff, pp, 0, P, K);
+        constexpr int KS = IL ? 4 : 1;  // stride of consecutive lags
         const int k1 = lane, k2 = lane + 64;
-        const int64_t v1 = k1 < K ? sc[k1] : 0, v2 = k2 < K ? sc[k2] : 0;
+        const int64_t v1 = k1 < K ? sc[KS * k1] : 0, v2 = k2 < K ? sc[KS * k2] : 0;
         uint64_t key = k1 < K ? vkey<7>(v1, k1) : 0;
         if (k2 < K) {
             const uint64_t k2k = vkey<7>(v2, k2);
@@ -204,13 +137,13 @@ __device__ void argmax_prior_mf(const tdoa_kparams &kp, int64_t *scores, int *be
         if (k1 < K) {
             const int d = k1 > bk ? k1 - bk : bk - k1;
             const int64_t wv = apply_prior(v1, prior[d]);
-            sc[k1] = wv;
+            sc[KS * k1] = wv;
             store_score(out, gbase + k1, v1, wv);
         }
         if (k2 < K) {
             const int d = k2 > bk ? k2 - bk : bk - k2;
             const int64_t wv = apply_prior(v2, prior[d]);
-            sc[k2] = wv;
+            sc[KS * k2] = wv;
             store_score(out, gbase + k2, v2, wv);
         }
         if (lane == 0) {
@@ -245,14 +178,16 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 #pragma unroll
     for (int r = 0; r < GR; r++) {
         if (tid + r * nt < U) {
-            int64_t L[4] = {0, 0, 0, 0};
+            // frame-interleaved table: the slot's four frames in two 16-B reads
+            typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+            i64x2 L01 = {0, 0}, L23 = {0, 0};
             for (int p = 0; p < P; p++) {
-                const int idx = p * K + ((q[r] >> (8 * p)) & 0xFFu);
-#pragma unroll
-                for (int f = 0; f < 4; f++)
-                    if (f < nf)
-                        L[f] += scores[f * P * K + idx];
+                const i64x2 *sl = reinterpret_cast<const i64x2 *>(
+                    scores + sidx<true>(0, p, (q[r] >> (8 * p)) & 0xFFu, P, K));
+                L01 += sl[0];
+                L23 += sl[1];
             }
+            const int64_t L[4] = {L01.x, L01.y, L23.x, L23.y};
 #pragma unroll
             for (int f = 0; f < 4; f++) {
                 const uint64_t k = vkey<14>(L[f], cl[r]);
@@ -453,6 +388,7 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
         const uint32_t *ra = sm.X + rowa * RS + kp.PADW;  // word of sample 0
         const uint32_t *rb = sm.X + rowb * RS + kp.PADW;
         v4i_mf hh = {0, 0, 0, 0}, xx = {0, 0, 0, 0}, ll = {0, 0, 0, 0};
+#pragma unroll 2
         for (int beta = 0; beta < NB; beta++) {
             // A: samples q0 .. q0 + 15, q0 = 64 beta + 16 g - w (w = r; may be odd / negative)
             const int q0 = 64 * beta + 16 * g - r;
@@ -482,18 +418,19 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
             const int d = r - n0;
             const int sb = rsum[4 * rowb] - (d > 0 ? rsum[4 * rowb + d] : 0);
             const int64_t corr = 128 * ((int64_t)rsum[4 * rowa] + sb) - (int64_t)16384 * 64 * NB;
-            int64_t *dst = sm.scores + (size_t)(f * P + p) * K + S;
+            int64_t *dst = sm.scores + sidx<KEYGRID>(f, p, S, P, K);
+            constexpr int KS = KEYGRID ? 4 : 1;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int sl = 16 * (r - n0) + 4 * g + e;
                 if (sl >= -S && sl <= S)
-                    dst[sl] = (int64_t)hh[e] * 65536 + (int64_t)xx[e] * 256 + (int64_t)ll[e] + corr;
+                    dst[KS * sl] = (int64_t)hh[e] * 65536 + (int64_t)xx[e] * 256 + (int64_t)ll[e] + corr;
             }
         }
     }
     __syncthreads();
     DIAG_STAMP(3);
-    argmax_prior_mf(kp, sm.scores, sm.best, reinterpret_cast<const float *>(smem + tb.prior), out, f0, nf);
+    argmax_prior_mf<KEYGRID>(kp, sm.scores, sm.best, reinterpret_cast<const float *>(smem + tb.prior), out, f0, nf);
     DIAG_STAMP(4);
     // grid solve (vga_heatmap.h:99-108) on the weighted scores still in LDS:
     // no [B][P][K] round trip through HBM and no second launch
@@ -727,8 +664,9 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         o += (size_t)128 * 4;
         tb.red = (int)o;
         o += (size_t)16 * 4 * 8;
-        // single-word tuples: each thread holds <= 4 of the grid's tuples
-        if (kp.TW == 1 && kp.U > 4 * threads)
+        // single-word tuples: each thread holds <= 4 of the grid's tuples, and
+        // the score table is frame-interleaved for exactly four frames
+        if (kp.TW == 1 && (kp.U > 4 * threads || kp.F != 4))
             return tdoa_set_error(-1, "DIRECT: more distinct lag tuples than the grid solve holds");
         const size_t lds = (o + 15) & ~(size_t)15;
         if (lds > 160 * 1024)

@@ -31,6 +31,7 @@
 #include <cstdlib>
 
 #include "tdoa_internal.h"
+#include "tdoa_keys.h"
 
 int tdoa_set_error(int code, const char *msg);
 
@@ -593,6 +594,7 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
     int64_t *W = (int64_t *)smem;     // [P][K] EMA scores
     __shared__ int64_t redv[TPB / 64];
     __shared__ int redi[TPB / 64];
+    __shared__ uint64_t redk[TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = TPB / 64;
     const int K = kp.K, P = kp.P;
     const int cnt = *sp.count;
@@ -646,8 +648,9 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
         int64_t *est = sp.est + (size_t)s * P * K;
         const int64_t *fr = sp.fresh + (size_t)slot * P * K;
         for (int p = wave; p < P; p += nwaves) {
-            int64_t bv = INT64_MIN;
-            int bk = INT_MAX;
+            // EMA of correlations.c:38-63, then the first maximum as a DPP key
+            // reduction (tdoa_keys.h: |EMA| <= 2^42 < 2^47)
+            uint64_t key = 0;
             for (int k = lane; k < 128; k += 64) {
                 if (k < K) {
                     const int64_t ev = est[p * K + k];
@@ -656,20 +659,11 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
                     const int64_t nv = (int64_t)sum;
                     est[p * K + k] = nv;
                     W[p * K + k] = nv;
-                    if (nv > bv) {
-                        bv = nv;
-                        bk = k;
-                    }
+                    const uint64_t kk = vkey<7>(nv, k);
+                    key = kk > key ? kk : key;
                 }
             }
-            for (int m = 32; m >= 1; m >>= 1) {
-                const int64_t ov = __shfl_xor(bv, m, 64);
-                const int ok = __shfl_xor(bk, m, 64);
-                if (ov > bv || (ov == bv && ok < bk)) {
-                    bv = ov;
-                    bk = ok;
-                }
-            }
+            const int bk = key_index<7>(lane63_u64(wave_umax_dpp(key)));
             if (lane == 0 && out.ema_best)
                 out.ema_best[(size_t)slot * P + p] = bk - kp.S;
         }
@@ -720,25 +714,18 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
                 }
             }
         }
-        for (int m = 32; m >= 1; m >>= 1) {
-            const int64_t ov = __shfl_xor(bv, m, 64);
-            const int ou = __shfl_xor(bu, m, 64);
-            if (ov > bv || (ov == bv && ou < bu)) {
-                bv = ov;
-                bu = ou;
-            }
-        }
-        if (lane == 0) {
-            redv[wave] = bv;
-            redi[wave] = bu;
-        }
+        // (L, first tuple) as one key (tdoa_keys.h; U < 2^14): DPP over the
+        // wave, LDS over the waves.  A thread without tuples keeps key 0.
+        uint64_t key = bu < kp.U ? vkey<14>(bv, bu) : 0;
+        key = wave_umax_dpp(key);
+        if (lane == 63)
+            redk[wave] = key;
         __syncthreads();
         if (tid == 0) {
-            for (int w = 1; w < nwaves; w++)
-                if (redv[w] > bv || (redv[w] == bv && redi[w] < bu)) {
-                    bv = redv[w];
-                    bu = redi[w];
-                }
+            for (int w = 0; w < nwaves; w++)
+                key = redk[w] > key ? redk[w] : key;
+            bv = key_value<14>(key);
+            bu = key_index<14>(key);
             if (bu < 0 || bu >= kp.U)
                 bu = 0;
             const int cell = kp.tuple_cell[bu];
