@@ -463,6 +463,9 @@ __global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params 
             const int b = i * M + m;
             return (int)((x[r][b >> 2] >> (8 * (b & 3))) & 0xFFu);
         };
+        // exclusive prefix sums over the lanes' chunks of each row: per mic the
+        // samples (v_dot4 of the chunk's words with a 0/1 byte mask of that
+        // mic's bytes), over all mics their squares (v_dot4 of a word with itself)
         int q1[3][M], q2[3];
         {
             int tot1[M], tot2 = 0;
@@ -471,55 +474,72 @@ __global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params 
                 tot1[m] = 0;
 #pragma unroll
             for (int r = 0; r < 3; r++) {
-                int c2 = 0;
+                uint32_t c2 = 0;
+#pragma unroll
+                for (int k = 0; k < CW; k++)
+                    c2 = __builtin_amdgcn_udot4(x[r][k], x[r][k], c2, false);
 #pragma unroll
                 for (int m = 0; m < M; m++) {
-                    int c1 = 0;
+                    uint32_t c1 = 0;
 #pragma unroll
-                    for (int i = 0; i < G; i++) {
-                        const int v = smp(r, i, m);
-                        c1 += v;
-                        c2 += v * v;
+                    for (int k = 0; k < CW; k++) {
+                        uint32_t mask = 0;  // bytes 4k + j of the chunk that are mic m's
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            mask |= ((4 * k + j) % M == m ? 1u : 0u) << (8 * j);
+                        c1 = __builtin_amdgcn_udot4(x[r][k], mask, c1, false);
                     }
-                    const int inc = wave_scan_incl(c1);
-                    q1[r][m] = tot1[m] + inc - c1;
+                    const int inc = wave_scan_incl((int)c1);
+                    q1[r][m] = tot1[m] + inc - (int)c1;
                     tot1[m] += __builtin_amdgcn_readlane(inc, 63);
                 }
-                const int inc2 = wave_scan_incl(c2);
-                q2[r] = tot2 + inc2 - c2;
+                const int inc2 = wave_scan_incl((int)c2);
+                q2[r] = tot2 + inc2 - (int)c2;
                 tot2 += __builtin_amdgcn_readlane(inc2, 63);
             }
         }
         // the words re-enter here opaque: the scan re-extracts the samples
-        // instead of keeping the prefix pass's 3 G M extracted bytes live
+        // instead of keeping the prefix pass's extracted bytes live
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll
             for (int k = 0; k < CW; k++)
                 asm volatile("" : "+v"(x[r][k]));
         const int64_t amin = rs + N - pos - 1;  // full ring: >= N samples since the last trigger
+        // the trigger of sample_compute.h:75-91 in difference form: with the
+        // older / newer half-window sums so, si per mic and D2 = (q2[1] - q2[0])
+        // - (q2[2] - q2[1]) of the squares, pout - pin = (D2 << hb) -
+        // sum_m (so - si)(so + si) -- pout > thr + pin exactly as the
+        // reference's int64 powers (rolling_buffer.c:73-85), one 64-bit
+        // multiply-add per mic instead of two squares
+        int so[M], si[M];
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            so[m] = q1[1][m] - q1[0][m];
+            si[m] = q1[2][m] - q1[1][m];
+        }
+        int D2 = (q2[1] - q2[0]) - (q2[2] - q2[1]);
         int fi = -1;
 #pragma unroll
         for (int i = 0; i < G; i++) {
             const int a = G * lane + i;
-            long long pout = (long long)(q2[1] - q2[0]) << hb, pin = (long long)(q2[2] - q2[1]) << hb;
+            long long T = (long long)D2 << hb;
+#pragma unroll
+            for (int m = 0; m < M; m++)
+                T -= (long long)(so[m] - si[m]) * (long long)(so[m] + si[m]);
+            if (fi < 0 && a >= amin && T > thr)
+                fi = i;
+            int w0 = 0, w1 = 0, w2 = 0;
 #pragma unroll
             for (int m = 0; m < M; m++) {
-                const long long so1 = q1[1][m] - q1[0][m], si1 = q1[2][m] - q1[1][m];
-                pout -= so1 * so1;
-                pin -= si1 * si1;
+                const int v0 = smp(0, i, m), v1 = smp(1, i, m), v2 = smp(2, i, m);
+                so[m] += v1 - v0;
+                si[m] += v2 - v1;
+                w0 += v0 * v0;
+                w1 += v1 * v1;
+                w2 += v2 * v2;
             }
-            if (fi < 0 && a >= amin && pout > thr + pin)
-                fi = i;
-#pragma unroll
-            for (int r = 0; r < 3; r++) {
-#pragma unroll
-                for (int m = 0; m < M; m++) {
-                    const int v = smp(r, i, m);
-                    q1[r][m] += v;
-                    q2[r] += v * v;
-                }
-            }
+            D2 += (w1 - w0) - (w2 - w1);
         }
         const uint64_t fire = have ? __ballot(fi >= 0) : 0;
         if (fire != 0) {
