@@ -46,8 +46,13 @@ from tdoa import shard  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak
 
-# BASELINE.json configs 2-5.  batch: per GPU (weak) or global (strong).
+# BASELINE.json configs 1-5.  batch: per GPU (weak) or global (strong).
 CONFIGS = {
+    # config 1: the reference's per-frame plumbing, 2 mics, through the
+    # reference-named entry points (one GPU-backed call per stage and buffer)
+    1: dict(desc="BASELINE config 1: 2-mic, 1024-sample frames, time-domain cross-correlation through the "
+                 "reference-named per-frame entry points (sample_compute.h:105-122 for one pair)",
+            M=2, N=1024, mics="two", batch=1, scaling="weak"),
     2: dict(desc="BASELINE config 2: 3-mic triangle, 1024-sample frames", M=3, N=1024,
             mics=None, batch=4096, scaling="weak"),
     3: dict(desc="BASELINE config 3: 4-mic square (0.15 m), 4096-sample frames, 6 pairs",
@@ -105,11 +110,11 @@ def parse():
     if a.batch is None:
         a.batch = cfg["batch"]
     if a.steps is None:
-        a.steps = {2: 400, 5: 200, 4: 5}.get(a.config, 20)
+        a.steps = {1: 200, 2: 400, 5: 200, 4: 5}.get(a.config, 20)
     if a.warmup is None:
-        a.warmup = {2: 20, 5: 20, 4: 2}.get(a.config, 3)
-    if a.config == 5:
-        a.engine = "direct"  # the streaming loop runs the reference's DIRECT path
+        a.warmup = {1: 10, 2: 20, 5: 20, 4: 2}.get(a.config, 3)
+    if a.config in (1, 5):
+        a.engine = "direct"  # the reference's integer path (per frame / streaming)
     return a
 
 
@@ -119,6 +124,8 @@ def config_mics(cfg):
         return synth.square_mics(0.15)
     if cfg["mics"] == "circle":
         return synth.circle_mics(cfg["M"], 0.15)
+    if cfg["mics"] == "two":
+        return np.array([[-0.066, 0.0], [0.066, 0.0]], np.float32)
     return None
 
 
@@ -276,6 +283,118 @@ def time_stream(args, dev, ri, cache):
                                    "measured after the timed region"}}
 
 
+def time_config1(args, dev, ri):
+    """Config 1: one 2-mic frame per step through the reference-named entry
+    points of tdoa_reference_abi.h -- rolling_buffer_write_out, buffer_normalize_range,
+    buffer_window for both buffers, then correlations_init (sample_compute.h:105-122
+    for one pair): seven GPU-backed per-frame calls, each a synchronous round trip
+    of the reference struct.  Every frame's correlations and best shift are checked
+    against the oracle after the timed region."""
+    import ctypes as C
+    import tdoa
+    from tdoa import _lib, synth
+    from tdoa.localizer import Localizer
+    cfg = CONFIGS[1]
+    L = tdoa.load()
+    if L.tdoa_ref_set_device(int(dev.index)) != 0:
+        raise RuntimeError("tdoa_ref_set_device failed")
+    loc = Localizer(engine="direct", num_mics=2, frame_len=1024, mic_xy=config_mics(cfg),
+                    device=dev.index)
+    S = loc.dims.S
+    win = loc.window()
+    n = args.steps + args.warmup
+    fr, _, _ = synth.adc_frames(n, 2, 1024, loc.lut(), S, shard.frame_seed(0x5EED0001, ri.rank))
+    fr = fr.numpy()
+    loc.close()
+    # the two rolling buffers of each frame: full rings, head 0 (oldest first)
+    rings = []
+    for i in range(n):
+        pair = []
+        for m in range(2):
+            rb = _lib.RollingBuffer()
+            rb.head, rb.is_full = 0, True
+            C.memmove(rb.buffer, np.ascontiguousarray(fr[i, m]).ctypes.data, 2048)
+            pair.append(rb)
+        rings.append(pair)
+    outs = [_lib.Correlations() for _ in range(n)]
+    ba, bb = _lib.Buffer(), _lib.Buffer()
+
+    def step(i):
+        ra, rb = rings[i]
+        L.rolling_buffer_write_out(C.byref(ra), C.byref(ba))
+        L.rolling_buffer_write_out(C.byref(rb), C.byref(bb))
+        L.buffer_normalize_range(C.byref(ba))
+        L.buffer_normalize_range(C.byref(bb))
+        L.buffer_window(C.byref(ba))
+        L.buffer_window(C.byref(bb))
+        L.correlations_init(C.byref(outs[i]), C.byref(ba), C.byref(bb))
+
+    for i in range(args.warmup):
+        step(i)
+    t = shard.timed(lambda k: step(args.warmup + k), args.steps, 0,
+                    sync=lambda: torch.cuda.synchronize(dev), device=dev)
+    total = shard.sum_over_ranks([args.steps], device=dev)[0]
+    # parity: the oracle's DC removal / normalise / window / xcorr / prior per frame
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    ok = 0
+    for i in range(args.warmup, n):
+        pre = [O.window(O.normalize(O.dc_remove(fr[i, m])[0]), win) for m in range(2)]
+        sc, best = O.xcorr(pre[0], pre[1], S)
+        got = np.frombuffer(bytes(outs[i].correlations), np.int64)
+        ok += int(outs[i].best_shift == best and (got == O.prior(sc, best)).all())
+    return {"value": total / t["wall_max_s"], "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
+            "parity": {"frames": args.steps, "bit_exact_frames": ok,
+                       "contract": "correlations (int64, after the lag prior) and best_shift equal "
+                                   "the oracle's for every timed frame"},
+            "S": S, "win": win, "frames": fr}
+
+
+def cpu_baseline_config1(args, res):
+    """The same per-frame sequence on one host core (the oracle's C port)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    fr, win, S = res["frames"], res["win"], res["S"]
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(args.cpu_seconds, 5.0):
+        f = fr[n % fr.shape[0]]
+        pre = [O.window(O.normalize(O.dc_remove(f[m])[0]), win) for m in range(2)]
+        sc, best = O.xcorr(pre[0], pre[1], S)
+        O.prior(sc, best)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "localizations/s", **_cpu_info(1),
+            "threads_source": "one thread (the per-frame path is sequential)", "kind": "port",
+            "sample": f"{n} 2-mic frames in {dt:.1f} s: oracle/tdoa_oracle.c dc_remove, normalize, "
+                      "window, xcorr, prior per frame (rolling_buffer.c, buffer.c, correlations.c), "
+                      "one thread, called from Python like the GPU path"}
+
+
+def main_config1(args, dev, ri):
+    res = time_config1(args, dev, ri)
+    world = shard.ranks_seen()
+    if ri.rank == 0:
+        cfg = CONFIGS[1]
+        line = {
+            "metric": "localizations/sec (2-mic DIRECT xcorr, reference per-frame entry points)",
+            "value": res["value"], "unit": "localizations/s", "n_gpus": world, "ranks_seen": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int16->int64",
+            "data": "synthetic (ADC-like u8 frames, injected integer delays) in host rolling-buffer "
+                    "structs, as the reference's capture side leaves them",
+            "config": {"workload": f"{cfg['desc']}, one frame per step", "mics": 2, "frame_len": 1024,
+                       "calls_per_frame": 7, "parallelism": f"dp{world} (per-frame, no collective)"},
+            "parity": res["parity"],
+            "roofline": None,
+            "note": "latency-bound plumbing: seven synchronous GPU-backed calls per frame "
+                    "(the batched API is configs 2-5)",
+            "cpu_baseline": cpu_baseline_config1(args, res) if world == 1 and not args.no_cpu else None,
+        }
+        print(json.dumps(line), flush=True)
+    shard.finalize()
+
+
 def _cpu_info(threads):
     model = platform.processor() or ""
     try:
@@ -371,6 +490,23 @@ def traffic_entry(args):
     return sum(per), src
 
 
+def stream_traffic(args):
+    """Config 5: HBM bytes per hop of the hop's kernels (trigger, DIRECT on the
+    triggered batch, update) from the committed PMC passes."""
+    try:
+        e = json.load(open(args.traffic_json)).get("c5_direct") or {}
+    except (OSError, ValueError):
+        return None, None
+    ks = e.get("kernels", {})
+    names = ("k_stream_trigger_p", "k_direct_mfma", "k_stream_update")
+    per = [sum(v["hbm_bytes"] for k, v in ks.items() if k.split("<")[0] == n) for n in names]
+    if not all(per):
+        return None, None
+    return sum(per), (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / "
+                      f"WRITE_SIZE passes on {' + '.join(names)} ({e.get('date', 'undated')}), "
+                      "read = 2 x FETCH_SIZE; the trigger re-reads the two previous hops")
+
+
 def main():
     args = parse()
     ri = shard.init_distributed("nccl")
@@ -379,6 +515,8 @@ def main():
     cache = {}
     if args.config == 5:
         return main_stream(args, dev, ri, cache)
+    if args.config == 1:
+        return main_config1(args, dev, ri)
     main_res = time_engine(args.engine, args, dev, ri, cache)
     other = None
     if args.also:
@@ -471,7 +609,7 @@ def main_stream(args, dev, ri, cache):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": res["capture_bytes_per_step"] / ri.world / (res["kernel_ms"] * 1e-3) / 1e9
                          / HBM_PEAK_GBS,
-                         "traffic": None, "traffic_source": None,
+                         **dict(zip(("traffic", "traffic_source"), stream_traffic(args))),
                          "kernel": "all kernels of a hop (hipGraph)", "kernel_ms": res["kernel_ms"],
                          "bytes_per_step": res["capture_bytes_per_step"] // ri.world},
             "cpu_baseline": None,
