@@ -365,12 +365,15 @@ __global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp,
 // wave kernel waited on its loads at the start of every wave: 68 % of wave
 // cycles in SQ_WAIT_ANY).  A firing stream's frame is written from the words
 // the wave already holds, staged through LDS (no second read of the ring).
+#ifndef TRIG_NWB
+#define TRIG_NWB 4  // waves per workgroup: occupancy in steps of one wave per SIMD
+#endif
 template <int G, int M>
-__global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
+__global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
 {
     constexpr int H = 64 * G, N = 2 * H, CB = G * M, CW = CB / 4;
     static_assert(CB % 4 == 0, "a lane's chunk is whole words");
-    constexpr int NWB = 8;  // waves per workgroup
+    constexpr int NWB = TRIG_NWB;  // waves per workgroup
     extern __shared__ __attribute__((aligned(16))) uint32_t stage_all[];  // [NWB waves][3 H M / 4]
     __shared__ int nfired[NWB], slot_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -432,23 +435,24 @@ __global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params 
 #pragma unroll
                 for (int k = 0; k < CW; k++)
                     x[r][k] = __builtin_amdgcn_alignbyte(wc[r][k + 1], wc[r][k], shc[r]);
-            } else {  // stream start (zeros) or the ring's end
+            } else {  // stream start (zeros) or the ring's end: byte by byte through
+                // the wave's stage (a compact loop: this rare path must not set
+                // the kernel's register count)
                 const int64_t l0 = base + r * H + G * lane;
-#pragma unroll
-                for (int k = 0; k < CW; k++)
-                    x[r][k] = 0;
-#pragma unroll
-                for (int i = 0; i < G; i++) {
+                uint8_t *sb8 = reinterpret_cast<uint8_t *>(stage) + r * H * M + lane * CB;
+                __builtin_amdgcn_wave_barrier();  // the previous stream's stage reads come first
+#pragma unroll 1
+                for (int b = 0; b < CB; b++) {
+                    const int i = b / M, m = b - i * M;
                     int64_t ji = jr[r] + i;
                     if (ji >= cl)
                         ji -= cl;
-#pragma unroll
-                    for (int m = 0; m < M; m++) {
-                        const int b = i * M + m;
-                        const uint32_t v = l0 + i < 0 ? 0u : (uint32_t)cap[(size_t)ji * M + m];
-                        x[r][b >> 2] |= v << (8 * (b & 3));
-                    }
+                    sb8[b] = l0 + i < 0 ? (uint8_t)0 : cap[(size_t)ji * M + m];
                 }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = 0; k < CW; k++)
+                    x[r][k] = stage[r * (H * M / 4) + lane * CW + k];
             }
         }
         // the next stream's words into the same registers, in flight while
@@ -522,6 +526,13 @@ __global__ void __launch_bounds__(512, 1) k_stream_trigger_p(tdoa_stream_params 
         int fi = -1;
 #pragma unroll
         for (int i = 0; i < G; i++) {
+            // sample i's words re-enter opaque: their bytes are extracted here,
+            // not hoisted for every i at once (registers: occupancy)
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int k = (i * M) >> 2; k <= (i * M + M - 1) >> 2; k++)
+                    asm volatile("" : "+v"(x[r][k]));
             const int a = G * lane + i;
             long long T = (long long)D2 << hb;
 #pragma unroll
@@ -796,16 +807,17 @@ static bool trigger_p_applies(const tdoa_stream_params &sp, int64_t S, int *res_
 template <int G, int M>
 static void launch_trigger_p(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
 {
-    const size_t lds = (size_t)8 * 3 * 64 * G * M;
-    const int res = tdoa_resident_blocks((const void *)k_stream_trigger_p<G, M>, 512, lds);
-    int64_t grid = (S + 7) / 8;
+    constexpr int NWB = TRIG_NWB;
+    const size_t lds = (size_t)NWB * 3 * 64 * G * M;
+    const int res = tdoa_resident_blocks((const void *)k_stream_trigger_p<G, M>, 64 * NWB, lds);
+    int64_t grid = (S + NWB - 1) / NWB;
     if (res > 0 && grid > res)
         grid = res;
     // a wave lists at most 64 triggered streams (one per lane): <= 64 per wave
-    const int64_t min_grid = (S + 8 * 64 - 1) / (8 * 64);
+    const int64_t min_grid = (S + NWB * 64 - 1) / (NWB * 64);
     if (grid < min_grid)
         grid = min_grid;
-    hipLaunchKernelGGL((k_stream_trigger_p<G, M>), dim3((unsigned)grid), dim3(512), lds, st, sp, S);
+    hipLaunchKernelGGL((k_stream_trigger_p<G, M>), dim3((unsigned)grid), dim3(64 * NWB), lds, st, sp, S);
 }
 
 template <int G>
