@@ -664,10 +664,10 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         o += (size_t)128 * 4;
         tb.red = (int)o;
         o += (size_t)16 * 4 * 8;
-        // single-word tuples: each thread holds <= 4 of the grid's tuples, and
-        // the score table is frame-interleaved for exactly four frames
-        if (kp.TW == 1 && (kp.U > 4 * threads || kp.F != 4))
-            return tdoa_set_error(-1, "DIRECT: more distinct lag tuples than the grid solve holds");
+        // the keyed grid (TWC = 1): single-word tuples, <= 4 per thread held in
+        // registers, the score table frame-interleaved for four frames; other
+        // shapes (wide geometries with more tuples) take the generic grid
+        const bool keyed = kp.TW == 1 && kp.U <= 4 * threads && kp.F == 4;
         const size_t lds = (o + 15) & ~(size_t)15;
         if (lds > 160 * 1024)
             return tdoa_set_error(-1, "DIRECT: shape needs more than 160 KiB LDS per workgroup");
@@ -693,7 +693,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         else                              \
             TDOA_LAUNCH_MF(PREP, TWC, 8); \
     } while (0)
-        if (kp.TW == 1) {
+        if (keyed) {
             if (prepared)
                 TDOA_LAUNCH_MF_CH(true, 1);
             else

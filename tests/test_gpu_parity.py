@@ -97,6 +97,9 @@ CONFIGS = [
     (4, 4096, 50000, 0, synth.square_mics(0.15), 50),
     (8, 2048, 50000, 0, synth.circle_mics(8, 0.15), 50),
     (5, 2048, 50000, 63, synth.circle_mics(5, 0.3), 30),
+    # 3 mics, S = 63, a triangle twice the reference's: 6510 distinct lag tuples,
+    # more than the keyed grid holds in registers (the generic grid solve)
+    (3, 1024, 67600, 63, np.array([[-0.132, -0.076], [0.132, -0.076], [0.0, 0.152]], np.float32), 50),
 ]
 
 
