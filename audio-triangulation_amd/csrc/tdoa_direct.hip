@@ -190,7 +190,7 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
             const int64_t L[4] = {L01.x, L01.y, L23.x, L23.y};
 #pragma unroll
             for (int f = 0; f < 4; f++) {
-                const uint64_t k = vkey<14>(L[f], cl[r]);
+                const uint64_t k = vkey<16>(L[f], cl[r]);
                 best[f] = k > best[f] ? k : best[f];
             }
         }
@@ -212,12 +212,12 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
             const uint64_t o = red[w * 4 + f];
             k = o > k ? o : k;
         }
-        const int cell = key_index<14>(k);
+        const int cell = key_index<16>(k);
         const int64_t fi = f0 + f;
         if (out.cell)
             out.cell[fi] = cell;
         if (out.max_L)
-            out.max_L[fi] = key_value<14>(k);
+            out.max_L[fi] = key_value<16>(k);
         if (out.xy) {
             const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
             out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
@@ -665,9 +665,10 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         tb.red = (int)o;
         o += (size_t)16 * 4 * 8;
         // the keyed grid (TWC = 1): single-word tuples, <= 4 per thread held in
-        // registers, the score table frame-interleaved for four frames; other
-        // shapes (wide geometries with more tuples) take the generic grid
-        const bool keyed = kp.TW == 1 && kp.U <= 4 * threads && kp.F == 4;
+        // registers, the score table frame-interleaved for four frames, cells in
+        // the key's 16 index bits; other shapes (wide geometries with more
+        // tuples, grids beyond 65536 cells) take the generic grid
+        const bool keyed = kp.TW == 1 && kp.U <= 4 * threads && kp.F == 4 && kp.G <= 65536;
         const size_t lds = (o + 15) & ~(size_t)15;
         if (lds > 160 * 1024)
             return tdoa_set_error(-1, "DIRECT: shape needs more than 160 KiB LDS per workgroup");

@@ -68,10 +68,11 @@ __device__ __forceinline__ uint64_t lane63_u64(uint64_t k)
 // Exact int64 (value, first index) maxima as one unsigned key: |score| <=
 // N * 2^30 <= 2^42 (N <= 4096) and |L| <= 28 * 2^42 < 2^47, so
 // key = (v + 2^47) << IB | (2^IB - 1 - index) orders by value, then by the
-// smaller index, in 48 + IB <= 62 bits.  Argmax: index = lag slot (IB = 7,
+// smaller index, in 48 + IB <= 64 bits.  Argmax: index = lag slot (IB = 7,
 // correlations.c:20-23 keeps the first maximum); grid: index = the tuple's
-// first cell (IB = 14) -- tuple order is first-cell order, so the smallest
-// cell among equal L is the first row-major argmax of vga_heatmap.h:99-108.
+// first cell or the tuple index (IB = 16, callers check < 65536) -- tuple
+// order is first-cell order, so the smallest cell among equal L is the first
+// row-major argmax of vga_heatmap.h:99-108.
 constexpr int64_t KEY_BIAS = (int64_t)1 << 47;
 template <int IB>
 __device__ __forceinline__ uint64_t vkey(int64_t v, int idx)

@@ -745,18 +745,42 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
                 }
             }
         }
-        // (L, first tuple) as one key (tdoa_keys.h; U < 2^14): DPP over the
-        // wave, LDS over the waves.  A thread without tuples keeps key 0.
-        uint64_t key = bu < kp.U ? vkey<14>(bv, bu) : 0;
-        key = wave_umax_dpp(key);
-        if (lane == 63)
-            redk[wave] = key;
+        if (kp.U < 65536) {
+            // (L, first tuple) as one key (tdoa_keys.h, 16 index bits): DPP over
+            // the wave, LDS over the waves.  A thread without tuples keeps key 0.
+            uint64_t key = bu < kp.U ? vkey<16>(bv, bu) : 0;
+            key = wave_umax_dpp(key);
+            if (lane == 63)
+                redk[wave] = key;
+        } else {
+            for (int m = 32; m >= 1; m >>= 1) {
+                const int64_t ov = __shfl_xor(bv, m, 64);
+                const int ou = __shfl_xor(bu, m, 64);
+                if (ov > bv || (ov == bv && ou < bu)) {
+                    bv = ov;
+                    bu = ou;
+                }
+            }
+            if (lane == 0) {
+                redv[wave] = bv;
+                redi[wave] = bu;
+            }
+        }
         __syncthreads();
         if (tid == 0) {
-            for (int w = 0; w < nwaves; w++)
-                key = redk[w] > key ? redk[w] : key;
-            bv = key_value<14>(key);
-            bu = key_index<14>(key);
+            if (kp.U < 65536) {
+                uint64_t key = 0;
+                for (int w = 0; w < nwaves; w++)
+                    key = redk[w] > key ? redk[w] : key;
+                bv = key_value<16>(key);
+                bu = key_index<16>(key);
+            } else {
+                for (int w = 1; w < nwaves; w++)
+                    if (redv[w] > bv || (redv[w] == bv && redi[w] < bu)) {
+                        bv = redv[w];
+                        bu = redi[w];
+                    }
+            }
             if (bu < 0 || bu >= kp.U)
                 bu = 0;
             const int cell = kp.tuple_cell[bu];

@@ -100,6 +100,8 @@ CONFIGS = [
     # 3 mics, S = 63, a triangle twice the reference's: 6510 distinct lag tuples,
     # more than the keyed grid holds in registers (the generic grid solve)
     (3, 1024, 67600, 63, np.array([[-0.132, -0.076], [0.132, -0.076], [0.0, 0.152]], np.float32), 50),
+    # a 261 x 261 grid: more cells than the keyed grid's 16 index bits
+    (3, 1024, 50000, 0, None, 130),
 ]
 
 
