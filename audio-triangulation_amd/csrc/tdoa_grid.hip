@@ -176,8 +176,36 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 
     for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
         __builtin_amdgcn_wave_barrier();  // the previous frame's reads of Wl come first
-        for (int e = lane; e < PK; e += 64)
-            Wl[e] = weighted[f * PK + e];
+        {
+            // the frame's P x K scores (10.4 KB at config 4): 16-B loads, eight per
+            // lane in flight before their LDS stores (one element per load and
+            // iteration waited on every load in turn: ~40 HBM round trips a frame)
+            const T *src = weighted + f * PK;
+            const int nv = (int)(((size_t)PK * sizeof(T)) / 16);
+            const bool vec = nv > 0 && (((uintptr_t)src | (uintptr_t)Wl) & 15) == 0;
+            int e0 = 0;
+            if (vec) {
+                const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+                uint4 *d4 = reinterpret_cast<uint4 *>(Wl);
+                for (int b = 0; b < nv; b += 8 * 64) {
+                    uint4 t[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {  // clamped: unconditional loads
+                        const int e = b + i * 64 + lane;
+                        t[i] = s4[e < nv ? e : nv - 1];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int e = b + i * 64 + lane;
+                        if (e < nv)
+                            d4[e] = t[i];
+                    }
+                }
+                e0 = nv * (int)(16 / sizeof(T));
+            }
+            for (int e = e0 + lane; e < PK; e += 64)
+                Wl[e] = src[e];
+        }
         __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
         T best;
         int bu;
