@@ -273,10 +273,18 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
     }
     // the prior: requested now, written once the frames have arrived
     const float pr = tid < kp.K ? kp.prior[tid] : 0.0f;
-    // pads are zero samples (offset form 0x0080 per sample); sums start at 0
-    for (int i = tid; i < rows * 2 * padw; i += nt) {
-        const int r = i / (2 * padw), k = i - r * 2 * padw;
-        sm.X[r * RS + (k < padw ? k : NW + k)] = 0x00800080u;
+    // each row as two byte planes of its offset-form samples z = x ^ 0x0080
+    // (plane 0: high bytes h = x >> 8, plane 1: low bytes l = (x & 255) - 128,
+    // both int8 -- the matrix cores' operands, read without any byte
+    // shuffles), RS words = 2 planes x (2 padw + N) bytes per row.  Pads are
+    // zero samples: h = 0x00, l = 0x80.
+    uint32_t *Xw = sm.X;
+    const int pdw = padw / 2;  // pad dwords per side and plane (2 padw samples)
+    const int PLD = RS / 2;    // dwords per plane
+    for (int i = tid; i < rows * 4 * pdw; i += nt) {
+        const int r = i / (4 * pdw), k = i - r * 4 * pdw;  // k: plane (k / 2pdw), side, dword
+        const int pl = k >= 2 * pdw, kk = k - pl * 2 * pdw;
+        Xw[r * RS + pl * PLD + (kk < pdw ? kk : NW / 2 + kk)] = pl ? 0x80808080u : 0u;
     }
     for (int i = tid; i < rows; i += nt)
         sm.sums[i] = 0;
@@ -334,7 +342,14 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
                 x.y ^= 0x00800080u;
                 x.z ^= 0x00800080u;
                 x.w ^= 0x00800080u;
-                *reinterpret_cast<uint4 *>(&sm.X[r * RS + padw + 4 * k]) = x;
+                // samples 8k .. 8k + 7: their high bytes and low bytes, 8 B per plane
+                const uint32_t h0 = __builtin_amdgcn_perm(x.y, x.x, 0x07050301u);
+                const uint32_t h1 = __builtin_amdgcn_perm(x.w, x.z, 0x07050301u);
+                const uint32_t l0 = __builtin_amdgcn_perm(x.y, x.x, 0x06040200u);
+                const uint32_t l1 = __builtin_amdgcn_perm(x.w, x.z, 0x06040200u);
+                uint32_t *rw = Xw + r * RS + pdw + 2 * k;
+                *reinterpret_cast<uint2 *>(rw) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2 *>(rw + PLD) = make_uint2(l0, l1);
             }
         }
     }
@@ -385,29 +400,35 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
     for (int it = wave; it < nf * P; it += nwaves) {
         const int f = it / P, p = it - f * P;
         const int rowa = f * kp.M + kp.pair_i[p], rowb = f * kp.M + kp.pair_j[p];
-        const uint32_t *ra = sm.X + rowa * RS + kp.PADW;  // word of sample 0
-        const uint32_t *rb = sm.X + rowb * RS + kp.PADW;
+        // byte planes (stage_mf): sample n's high byte at byte 2 padw + n of
+        // plane 0, its offset low byte at the same byte of plane 1
+        const char *ra = reinterpret_cast<const char *>(sm.X + rowa * RS) + 2 * kp.PADW;
+        const char *rb = reinterpret_cast<const char *>(sm.X + rowb * RS) + 2 * kp.PADW;
+        const int PLB = RS * 2;  // bytes per plane
         v4i_mf hh = {0, 0, 0, 0}, xx = {0, 0, 0, 0}, ll = {0, 0, 0, 0};
 #pragma unroll 2
         for (int beta = 0; beta < NB; beta++) {
-            // A: samples q0 .. q0 + 15, q0 = 64 beta + 16 g - w (w = r; may be odd / negative)
+            // A: samples q0 .. q0 + 15, q0 = 64 beta + 16 g - w (w = r; any alignment,
+            // may be negative): five aligned dwords per plane, byte-aligned in registers
             const int q0 = 64 * beta + 16 * g - r;
-            const int wa = q0 >> 1;
-            const uint32_t sh = (uint32_t)(q0 & 1) * 2u;
-            uint32_t u[9], aw[8], bw[8];
+            const uint32_t *pa = reinterpret_cast<const uint32_t *>(ra + (q0 & ~3));
+            const uint32_t sh = (uint32_t)(q0 & 3);
+            uint32_t uh[5], ul[5];
 #pragma unroll
-            for (int m = 0; m < 9; m++)
-                u[m] = ra[wa + m];
+            for (int m = 0; m < 5; m++) {
+                uh[m] = pa[m];
+                ul[m] = pa[PLB / 4 + m];
+            }
+            v4i_mf ah, al;
 #pragma unroll
-            for (int m = 0; m < 8; m++)
-                aw[m] = __builtin_amdgcn_alignbyte(u[m + 1], u[m], sh);
-            // B: samples 64 beta + 16 (g + n - n0) .. + 15 (even start)
-            const int wb = 32 * beta + 8 * (g + rr - n0);
-#pragma unroll
-            for (int m = 0; m < 8; m++)
-                bw[m] = rb[wb + m];
-            const v4i_mf ah = mf_limbs(aw, 0x07050301u), al = mf_limbs(aw, 0x06040200u);
-            const v4i_mf bh = mf_limbs(bw, 0x07050301u), bl = mf_limbs(bw, 0x06040200u);
+            for (int d = 0; d < 4; d++) {
+                ah[d] = (int)__builtin_amdgcn_alignbyte(uh[d + 1], uh[d], sh);
+                al[d] = (int)__builtin_amdgcn_alignbyte(ul[d + 1], ul[d], sh);
+            }
+            // B: samples 64 beta + 16 (g + n - n0) .. + 15: one aligned 16-B read per plane
+            const int qb = 64 * beta + 16 * (g + rr - n0);
+            const v4i_mf bh = *reinterpret_cast<const v4i_mf *>(rb + qb);
+            const v4i_mf bl = *reinterpret_cast<const v4i_mf *>(rb + PLB + qb);
             hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bh, hh, 0, 0, 0);
             xx = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bl, xx, 0, 0, 0);
             xx = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bh, xx, 0, 0, 0);
