@@ -482,6 +482,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = C + C / 16;
     static_assert(M >= 2 && M <= G, "one forward round: every mic has its own group");
     constexpr int P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G;
+    constexpr int WPG = T / 64;  // waves per group (4 or 2)
+    static_assert(WPG == 2 || WPG == 4, "group of 2 or 4 waves");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *bufs = (f2 *)smem;                    // [G][BUF]
     f2 *xhalf = bufs + G * BUF;               // [G] U_m[C / 2]
@@ -499,6 +501,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         ttl[threadIdx.x] = reinterpret_cast<const f2 *>(kp.r16_tw)[threadIdx.x];
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
+    const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
 #ifdef TDOA_DIAG
     unsigned long long stamp[16] = {};
     int nst = 0;
@@ -721,16 +724,23 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             sts2(buf, o + 48, x15);
         }
         __syncthreads();
-        // pass 3 by the group's first wave: one output per column
-        if (jl < 64 && pair_on) {
-            const int l = jl;
-            const int jc = l < 32 ? l : 192 + l;
+        // pass 3 by one wave of the group, one output per column.  Waves of a
+        // workgroup go to SIMD (wave index mod 4): the group's wave P3W lands
+        // the G pass-3 waves evenly on the four SIMDs (the group's first wave
+        // put them all on SIMD 0, or 0 and 2, one after another)
+        if ((jl >> 6) == P3W && pair_on) {
+            const int l = jl & 63;
             const int mm = 64 - l;
+            // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
+            // the output index C - m; one table product per term, conjugated for l < 32
+            const int xw = l < 32 ? l : mm;
+            const float cs = l < 32 ? -1.0f : 1.0f;
             f2 y = lds2(buf, l);
 #pragma unroll
             for (int r = 1; r < R1; r++) {
                 const f2 u = lds2(buf, 64 * r + l);
-                y = y + (l < 32 ? c_mulconj(u, twC(tt, r, jc)) : c_mul(u, twC(tt, r, mm)));
+                const f2 t = twC(tt, r, xw);
+                y = y + c_mul(u, f2{t.x, cs * t.y});
             }
             const int n = l < 32 ? l : -mm;
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
