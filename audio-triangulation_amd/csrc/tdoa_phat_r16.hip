@@ -687,19 +687,27 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const int p = p0 + g;
         const bool pair_on = p < P;
         // inverse pass 1 (radix 16, Ns = 1)
+        // a partial last round (P mod G pairs): the idle groups skip the
+        // transforms, leaving their SIMDs' issue slots to the busy groups
+        const bool on = p0 + G <= P || pair_on;
         f2 v[16];
+        if (on) {
 #pragma unroll
-        for (int r = 0; r < 16; r++)
-            v[r] = lds2(buf, jl + T * r);
-        dftp<16, true, false>(v);
+            for (int r = 0; r < 16; r++)
+                v[r] = lds2(buf, jl + T * r);
+            dftp<16, true, false>(v);
+        }
         __syncthreads();
+        if (on) {
 #pragma unroll
-        for (int r = 0; r < 16; r++)
-            sts2(buf, 16 * jl + r, v[brev<16>(r)]);
+            for (int r = 0; r < 16; r++)
+                sts2(buf, 16 * jl + r, v[brev<16>(r)]);
+        }
         __syncthreads();
         // pass 2: outputs r'' in {0, 1, 14, 15} only
         const int k = jl & 15;
         f2 x0 = f2{0, 0}, x1 = f2{0, 0}, x14 = f2{0, 0}, x15 = f2{0, 0};
+        if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
             f2 l0 = lds2(buf, jl + T * r), l1 = lds2(buf, jl + T * (r + 4));
@@ -716,7 +724,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             x15 = x15 + (r ? dif_tw<false>(d0, d1, 4 * r) : d0 - d1);
         }
         __syncthreads();
-        {
+        if (on) {
             const int o = (jl >> 4) * 64 + k;
             sts2(buf, o, x0);
             sts2(buf, o + 16, x1);
