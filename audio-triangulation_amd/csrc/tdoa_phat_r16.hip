@@ -490,6 +490,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     int *red = (int *)(xhalf + G);            // [16] per-wave DC partial sums
     int *lagl = red + 16;                     // [TDOA_MAX_PAIRS]
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
+    float *priorl = (float *)(ttl + 3 * 16 * 16);  // [128] the lag prior (K <= 127)
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -499,6 +500,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // barrier, where a global (L2) round trip would stall the whole workgroup
     if (threadIdx.x < 3 * 16 * 16)  // 8-B units: kp.r16_tw is 8-B aligned
         ttl[threadIdx.x] = reinterpret_cast<const f2 *>(kp.r16_tw)[threadIdx.x];
+    // the prior too: a pass-3 global read waits (vmcnt) for the next frame's
+    // words, requested just before the pair rounds
+    if (threadIdx.x < (unsigned)kp.K)
+        priorl[threadIdx.x] = kp.prior[threadIdx.x];
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
     const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
@@ -619,11 +624,19 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // split + unit normalisation of every mic at this thread's bin pairs:
     // X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), X[C-b] = conj(e + i W od)
     // (b = 0: its partner output is X[C])
+    // W_2C^b of this thread's bins (the split and every pair's pre-twiddle), W_2C^{C/2}
+    // (requested before the forward's last pass instead, they measured slower:
+    // 4.89 vs 4.71 ms per config-3 step)
+    f2 twb[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+        twb[s] = tw2[tid + 1024 * s];
+    const f2 twh = tw2[C / 2];
     f2 Ub[M][NS], Un[M][NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const int b = tid + 1024 * s;
-        const f2 wb = tw2[b];
+        const f2 wb = twb[s];
 #pragma unroll
         for (int m = 0; m < M; m++) {
             const f2 *zb = bufs + m * BUF;
@@ -634,11 +647,6 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             Un[m][s] = c_unit(c_conj_add_i(e, od), e2);
         }
     }
-    f2 twb[NS];  // W_2C^b of this thread's bins, for every pair's pre-twiddle
-#pragma unroll
-    for (int s = 0; s < NS; s++)
-        twb[s] = tw2[tid + 1024 * s];
-    const f2 twh = tw2[C / 2];
     if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
         const f2 zh = lds2(bufs + tid * BUF, C / 2);
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
@@ -773,14 +781,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 if (out.scores_f)
                     out.scores_f[gb + ka] = sa;
                 if (out.weighted_f)
-                    out.weighted_f[gb + ka] = sa * kp.prior[dd];
+                    out.weighted_f[gb + ka] = sa * priorl[dd];
             }
             if (okb) {
                 const int dd = kb > bk ? kb - bk : bk - kb;
                 if (out.scores_f)
                     out.scores_f[gb + kb] = sb;
                 if (out.weighted_f)
-                    out.weighted_f[gb + kb] = sb * kp.prior[dd];
+                    out.weighted_f[gb + kb] = sb * priorl[dd];
             }
             if (l == 0) {
                 out.lags[fr * P + p] = bk - S;
@@ -818,7 +826,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 {
     constexpr int G = 16384 / C, BUF = C + C / 16;
     const size_t lds = (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
-                       3 * 16 * 16 * sizeof(f2);
+                       3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float);
     if (B <= 0)
         return 0;
     const int res = tdoa_resident_blocks((const void *)k_frame16<C, M>, 1024, lds);
