@@ -49,6 +49,10 @@ template <int C>
 constexpr int r16_row() { return C + 32; }
 
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+// padded offset of o, a multiple of 16: pidx(i + o) == pidx(i) + po(o) -- the
+// k_frame16 accesses are a per-thread base plus compile-time offsets (folded
+// into the ds instruction) instead of a shift and add per access
+__host__ __device__ constexpr int po(int o) { return o + (o >> 4); }
 __device__ __forceinline__ f2 lds2(const f2 *buf, int i) { return buf[pidx(i)]; }
 __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 
@@ -527,7 +531,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     for (int64_t fr = blockIdx.x; fr < B; fr += gridDim.x) {
     // thread indices the compiler cannot prove loop-invariant: the passes'
     // twiddle reads stay in the body instead of being hoisted (and spilled)
-    const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T;
+    const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T, pj = pidx(j);
     if (fr == blockIdx.x)
         F16_MARK();
 
@@ -569,7 +573,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             dftp<16, false, true>(v);
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                sts2(buf, 16 * j + r, v[brev<16>(r)]);
+                buf[17 * j + r] = v[brev<16>(r)];  // pidx(16 j + r)
         } else {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -581,10 +585,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 for (int r = 4; r < 8; r++)
                     u[r] = f2{0.0f, 0.0f};
                 dftp<8, false, true>(u);
-                const int jv = j + 128 * h;
+                // pidx(8 (j + 128 h) + r) = 8 j + (j >> 1) + 1088 h + r (r < 8)
 #pragma unroll
                 for (int r = 0; r < 8; r++)
-                    sts2(buf, 8 * jv + r, u[brev<8>(r)]);
+                    buf[8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
             }
         }
         __syncthreads();
@@ -592,22 +596,23 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int k = j % R1;
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                v[r] = lds2(buf, j + T * r);
+                v[r] = buf[pj + po(T * r)];
 #pragma unroll
             for (int r = 1; r < 16; r++)
                 v[r] = c_mul(v[r], tw16h(tt, r, k));
             dftp<16, false, false>(v);
             __syncthreads();
-            const int o = (j / R1) * 16 * R1 + k;
+            // o mod 16 = k < R1: pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16
+            const int o = pidx((j / R1) * 16 * R1 + k);
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                sts2(buf, o + R1 * r, v[brev<16>(r)]);
+                buf[o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
         }
         __syncthreads();
         {
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                v[r] = lds2(buf, j + T * r);
+                v[r] = buf[pj + po(T * r)];
 #pragma unroll
             for (int r = 1; r < 16; r++)
                 v[r] = c_mul(v[r], twC(tt, r, j));
@@ -615,7 +620,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
-                sts2(buf, j + T * q, v[brev<16>(q)]);
+                buf[pj + po(T * q)] = v[brev<16>(q)];
         }
         __syncthreads();
     }
@@ -636,11 +641,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const int b = tid + 1024 * s;
+        const int pb = pidx(b), pp = pidx((C - b) & (C - 1));
         const f2 wb = twb[s];
 #pragma unroll
         for (int m = 0; m < M; m++) {
             const f2 *zb = bufs + m * BUF;
-            const f2 z = lds2(zb, b), zp = lds2(zb, (C - b) & (C - 1));
+            const f2 z = zb[pb], zp = zb[pp];
             const f2 e = c_addconj(z, zp);
             const f2 od = c_mul(c_subconj(z, zp), wb);
             Ub[m][s] = c_unit(c_add_mi(e, od), e2);
@@ -664,7 +670,16 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     const float invL = 1.0f / (float)(2 * C);
     static_for<0, ROUNDS>([&](auto rc) {
         constexpr int p0 = decltype(rc)::value * G;
-        const int tl = opaque_idx(tid), jl = tl - g * T;
+        const int tl = opaque_idx(tid), jl = tl - g * T, pjl = pidx(jl);
+        // this thread's Y slots b = tl + 1024 s and C - b (b = 0: C / 2, whose
+        // value thread 0 writes after, in program order)
+        int yb0[NS], yb1[NS];
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int b = tl + 1024 * s;
+            yb0[s] = pidx(b);
+            yb1[s] = b == 0 ? pidx(C / 2) : pidx(C - b);
+        }
         // packed inverse input Y of pair p0 + gg into buffer gg (all threads)
         static_for<0, G>([&](auto gc) {
             constexpr int pc = p0 + decltype(gc)::value;
@@ -673,14 +688,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 f2 *yb = bufs + decltype(gc)::value * BUF;
 #pragma unroll
                 for (int s = 0; s < NS; s++) {
-                    const int b = tl + 1024 * s;
                     const f2 Rk = c_conjmul(Ub[pi][s], Ub[pj][s]);  // R[b]
                     const f2 Rq = c_conjmul(Un[pi][s], Un[pj][s]);  // R[C-b]
                     const f2 ss = c_addconj(Rk, Rq);
                     const f2 qq = c_mulconj(c_subconj(Rk, Rq), twb[s]);
-                    sts2(yb, b, c_add_i(ss, qq));
-                    if (b != 0)
-                        sts2(yb, C - b, c_conj_add_mi(ss, qq));
+                    yb[yb0[s]] = c_add_i(ss, qq);
+                    yb[yb1[s]] = c_conj_add_mi(ss, qq);
                 }
                 if (tl == 0) {  // Y[C/2] from R[C/2] alone
                     const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
@@ -702,14 +715,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on) {
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                v[r] = lds2(buf, jl + T * r);
+                v[r] = buf[pjl + po(T * r)];
             dftp<16, true, false>(v);
         }
         __syncthreads();
         if (on) {
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                sts2(buf, 16 * jl + r, v[brev<16>(r)]);
+                buf[17 * jl + r] = v[brev<16>(r)];
         }
         __syncthreads();
         // pass 2: outputs r'' in {0, 1, 14, 15} only
@@ -718,9 +731,9 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
-            f2 l0 = lds2(buf, jl + T * r), l1 = lds2(buf, jl + T * (r + 4));
-            const f2 h0 = c_mulconj(lds2(buf, jl + T * (r + 8)), tw256(tt, r + 8, k));
-            const f2 h1 = c_mulconj(lds2(buf, jl + T * (r + 12)), tw256(tt, r + 12, k));
+            f2 l0 = buf[pjl + po(T * r)], l1 = buf[pjl + po(T * (r + 4))];
+            const f2 h0 = c_mulconj(buf[pjl + po(T * (r + 8))], tw256(tt, r + 8, k));
+            const f2 h1 = c_mulconj(buf[pjl + po(T * (r + 12))], tw256(tt, r + 12, k));
             if (r)
                 l0 = c_mulconj(l0, tw256(tt, r, k));
             l1 = c_mulconj(l1, tw256(tt, r + 4, k));
@@ -733,11 +746,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
         __syncthreads();
         if (on) {
-            const int o = (jl >> 4) * 64 + k;
-            sts2(buf, o, x0);
-            sts2(buf, o + 16, x1);
-            sts2(buf, o + 32, x14);
-            sts2(buf, o + 48, x15);
+            const int o = pidx((jl >> 4) * 64 + k);  // + po(16 c) = 17 c
+            buf[o] = x0;
+            buf[o + 17] = x1;
+            buf[o + 34] = x14;
+            buf[o + 51] = x15;
         }
         __syncthreads();
         // pass 3 by one wave of the group, one output per column.  Waves of a
@@ -751,10 +764,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             // the output index C - m; one table product per term, conjugated for l < 32
             const int xw = l < 32 ? l : mm;
             const float cs = l < 32 ? -1.0f : 1.0f;
-            f2 y = lds2(buf, l);
+            const int pl = pidx(l);
+            f2 y = buf[pl];
 #pragma unroll
             for (int r = 1; r < R1; r++) {
-                const f2 u = lds2(buf, 64 * r + l);
+                const f2 u = buf[pl + 68 * r];
                 const f2 t = twC(tt, r, xw);
                 y = y + c_mul(u, f2{t.x, cs * t.y});
             }
