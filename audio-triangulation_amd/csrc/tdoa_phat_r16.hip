@@ -37,6 +37,7 @@
 #define TDOA_ASM_MUL_S 1
 #include "tdoa_cplx.h"
 #include "tdoa_internal.h"
+#include "tdoa_keys.h"
 
 int tdoa_set_error(int code, const char *msg);
 
@@ -495,6 +496,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     int *lagl = red + 16;                     // [TDOA_MAX_PAIRS]
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
     float *priorl = (float *)(ttl + 3 * 16 * 16);  // [128] the lag prior (K <= 127)
+    f2 *tw3 = (f2 *)(priorl + 128);  // [R1][64] pass-3 twiddles per lane (row 0 unused)
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -508,6 +510,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // words, requested just before the pair rounds
     if (threadIdx.x < (unsigned)kp.K)
         priorl[threadIdx.x] = kp.prior[threadIdx.x];
+    // (pass 3 multiplied two table entries per term before: 4.51 vs 4.26 ms per config-3 step)
+    if (threadIdx.x < R1 * 64) {  // lane l: conj(W_C^{r l}) (l < 32), W_C^{r (64 - l)}
+        const int r = threadIdx.x >> 6, l = threadIdx.x & 63;
+        const f2 t = twC(reinterpret_cast<const f2 *>(kp.r16_tw), r, l < 32 ? l : 64 - l);
+        tw3[threadIdx.x] = f2{t.x, l < 32 ? -t.y : t.y};
+    }
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
     const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
@@ -545,10 +553,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
         for (int s = 0; s < 8; s++)
             sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_r16, w[s]), v2s_r16{1, 1}, sum, false);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1)
-            sum += __shfl_xor(sum, o, 64);
-        if ((tid & 63) == 0)
+        sum = group_sum_dpp(sum, 64);  // DPP moves to lane 63 (no LDS round trips)
+        if ((tid & 63) == 63)
             red[tid >> 6] = sum;
         __syncthreads();
         sum = 0;
@@ -761,16 +767,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int l = jl & 63;
             const int mm = 64 - l;
             // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
-            // the output index C - m; one table product per term, conjugated for l < 32
-            const int xw = l < 32 ? l : mm;
-            const float cs = l < 32 ? -1.0f : 1.0f;
+            // the output index C - m; tw3 holds each lane's factors (conjugated for l < 32)
             const int pl = pidx(l);
             f2 y = buf[pl];
 #pragma unroll
             for (int r = 1; r < R1; r++) {
                 const f2 u = buf[pl + 68 * r];
-                const f2 t = twC(tt, r, xw);
-                y = y + c_mul(u, f2{t.x, cs * t.y});
+                y = y + c_mul(u, tw3[64 * r + l]);
             }
             const int n = l < 32 ? l : -mm;
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
@@ -840,7 +843,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 {
     constexpr int G = 16384 / C, BUF = C + C / 16;
     const size_t lds = (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
-                       3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float);
+                       3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2);
     if (B <= 0)
         return 0;
     const int res = tdoa_resident_blocks((const void *)k_frame16<C, M>, 1024, lds);
