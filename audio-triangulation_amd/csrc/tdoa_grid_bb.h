@@ -54,6 +54,46 @@ __device__ __forceinline__ void better(T &bv, int &bu, T ov, int ou)
     }
 }
 
+// (max, first index) across the wave by DPP lane moves -> lane 63 (the
+// __shfl_xor butterfly was a chain of twelve LDS round trips per reduction):
+// xor 1, xor 2, half-row mirror, row mirror, row_bcast:15, row_bcast:31.
+// Lanes without a source keep their own value (old = src).
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_mov(int v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_mov(float v)
+{
+    return __builtin_bit_cast(float, dpp_mov<CTRL, RM>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ int64_t dpp_mov(int64_t v)
+{
+    const uint32_t lo = (uint32_t)dpp_mov<CTRL, RM>((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)dpp_mov<CTRL, RM>((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <int CTRL, int RM, typename T>
+__device__ __forceinline__ void dpp_better(T &v, int &i)
+{
+    better<T>(v, i, dpp_mov<CTRL, RM>(v), dpp_mov<CTRL, RM>(i));
+}
+// the wave's (max, first index) to every lane
+template <typename T>
+__device__ __forceinline__ void wave_best(T &v, int &i)
+{
+    dpp_better<0xB1, 0xF>(v, i);
+    dpp_better<0x4E, 0xF>(v, i);
+    dpp_better<0x141, 0xF>(v, i);
+    dpp_better<0x140, 0xF>(v, i);
+    dpp_better<0x142, 0xA>(v, i);
+    dpp_better<0x143, 0xC>(v, i);
+    v = readlane(v, 63);
+    i = __builtin_amdgcn_readlane(i, 63);
+}
+
 // One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
 // by this wave before the call); M8: a [128] LDS scratch row of this wave;
 // tiles / rng: the entry table (LDS or global).  Returns the max L (best) and
@@ -126,9 +166,8 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             sv = bt[j];
             st = lane + 64 * j;
         }
-    for (int m = 32; m >= 1; m >>= 1)
-        better<T>(sv, st, (T)__shfl_xor(sv, m, 64), __shfl_xor(st, m, 64));
-    const int seed = __builtin_amdgcn_readfirstlane(st);
+    wave_best<T>(sv, st);
+    const int seed = st;
 
     T best = low;
     int bu = INT_MAX;
@@ -160,10 +199,9 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             return;
         T v = win ? L : low;
         int vi = win ? ui : INT_MAX;
-        for (int m = 32; m >= 1; m >>= 1)
-            better<T>(v, vi, (T)__shfl_xor(v, m, 64), __shfl_xor(vi, m, 64));
-        best = readlane(v, 0);
-        bu = __builtin_amdgcn_readfirstlane(vi);
+        wave_best<T>(v, vi);
+        best = v;
+        bu = vi;
     };
     if (NT > 0)
         eval(seed);
