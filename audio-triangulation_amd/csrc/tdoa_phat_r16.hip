@@ -34,7 +34,9 @@
 
 // the long-frame kernels measured faster with the asm constant-twiddle
 // products (k_frame16<2048, 8>: 123.4 vs 127.4 ms per 1e6 frames)
+#ifndef R16_VEC_MUL_S
 #define TDOA_ASM_MUL_S 1
+#endif
 #include "tdoa_cplx.h"
 #include "tdoa_internal.h"
 #include "tdoa_keys.h"
