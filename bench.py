@@ -100,6 +100,10 @@ def parse():
     ap.add_argument("--rotate-mib", type=int, default=320,
                     help="frames rotated per rank (> 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--preflight-s", type=float, default=0.25,
+                    help="untimed steps for this long before the W warmups (configs 2-4): clocks and "
+                         "the rotating batches' translations settle, so a short K-step window "
+                         "measures the steady state; 0 disables")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--also", action="store_true", help="also time the other engine")
@@ -194,6 +198,16 @@ def time_engine(engine, args, dev, ri, cache):
         taus.append(tau)
     out = loc.alloc_outputs(B, grid=not args.no_grid)
     stream = torch.cuda.current_stream(dev)
+    # preflight (untimed, before the W warmups): every rotating batch once, then
+    # until preflight_s has passed (bounded); reported in the line
+    pre_n, pre_t0 = 0, time.perf_counter()
+    while args.preflight_s > 0 and (pre_n < R or time.perf_counter() - pre_t0 < args.preflight_s) \
+            and pre_n < 20000:
+        loc.localize_into(batches[pre_n % R], out, stream)
+        pre_n += 1
+        if pre_n % 64 == 0:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t = shard.timed(lambda k: loc.localize_into(batches[k % R], out, stream), args.steps,
@@ -212,6 +226,7 @@ def time_engine(engine, args, dev, ri, cache):
         "achieved_gbs": bytes_per_loc * B / kern_s / 1e9,
         "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
         "rotate_batches": R,
+        "preflight_steps": pre_n,
     }
     lags = out["lags"].cpu()
     assert int(lags.abs().max()) <= loc.dims.S
@@ -538,6 +553,9 @@ def main():
             "ranks_seen": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "preflight": {"steps": main_res["preflight_steps"], "seconds": args.preflight_s,
+                          "note": "untimed, before the warmups: every rotating batch once, then "
+                                  "steps until the time has passed"},
             "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": cfg["scaling"],
