@@ -1226,18 +1226,11 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         for (int i = 0; i < 4; i++)
             q[i] = tups[64 * i + lane64];
         gather(q, g);
-        for (int u0 = 0; u0 < Upad; u0 += 256) {
-            const int un = u0 + 256 < Upad ? u0 + 256 : u0;
-            uint32_t qn[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                qn[i] = tups[un + 64 * i + lane64];
-            f2 gn[4][3];
-            gather(qn, gn);
+        auto consume = [&](const f2 (&gg)[4][3], int ub) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const f2 Lg = (g[i][0] + g[i][1]) + g[i][2];
-                const int u = u0 + 64 * i + lane64;  // ascending per lane
+                const f2 Lg = (gg[i][0] + gg[i][1]) + gg[i][2];
+                const int u = ub + 64 * i + lane64;  // ascending per lane
                 if (Lg.x > gv[0]) {
                     gv[0] = Lg.x;
                     gu[0] = u;
@@ -1247,11 +1240,23 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                     gu[1] = u;
                 }
             }
+        };
+        // two steps per trip (Upad is a multiple of 512): the step buffers
+        // alternate instead of being copied back (24 moves a step)
+        for (int u0 = 0; u0 < Upad; u0 += 512) {
+            uint32_t qn[4];
 #pragma unroll
             for (int i = 0; i < 4; i++)
+                qn[i] = tups[u0 + 256 + 64 * i + lane64];
+            f2 gn[4][3];
+            gather(qn, gn);
+            consume(g, u0);
+            const int un = u0 + 512 < Upad ? u0 + 512 : u0 + 256;  // (a harmless re-read)
 #pragma unroll
-                for (int k = 0; k < 3; k++)
-                    g[i][k] = gn[i][k];
+            for (int i = 0; i < 4; i++)
+                q[i] = tups[un + 64 * i + lane64];
+            gather(q, g);
+            consume(gn, u0 + 256);
         }
         LEAN_MARK();
 #pragma unroll
