@@ -37,6 +37,8 @@ def test_defaults_are_the_headline_run():
     assert a.steps >= 100 and a.warmup >= 1
     assert _args("--config", "5").engine == "direct"
     assert _args("--config", "1").engine == "direct"
+    # the untimed preflight is on by default and can be switched off
+    assert a.preflight_s > 0 and _args("--preflight-s", "0").preflight_s == 0
 
 
 def test_traffic_only_for_dispatched_kernels():
