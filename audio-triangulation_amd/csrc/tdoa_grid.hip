@@ -154,6 +154,10 @@ __global__ void __launch_bounds__(1024) k_grid(tdoa_kparams kp, tdoa_kout out,
     }
 }
 
+#ifdef TDOA_DIAG
+__device__ unsigned long long g_diag_bb[8192 * 8];  // per-wave phase cycles (tdoa_grid_bb.h)
+#endif
+
 // ---------------------------------------------------------------------------
 // k_grid_bb: the same solve (max L, first argmax tuple) by exact branch and
 // bound, one wave per frame (tdoa_grid_bb.h).
@@ -174,7 +178,11 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
         rng[e] = kp.bb_rng[e];
     __syncthreads();
 
+    unsigned long long bbacc[8] = {};
     for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
+#ifdef TDOA_DIAG
+        const unsigned long long t_load = __builtin_amdgcn_s_memtime();
+#endif
         __builtin_amdgcn_wave_barrier();  // the previous frame's reads of Wl come first
         {
             // the frame's P x K scores (10.4 KB at config 4): 16-B loads, eight per
@@ -207,9 +215,17 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
                 Wl[e] = src[e];
         }
         __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+#ifdef TDOA_DIAG
+        {
+            // the loads' data reaches LDS (and so the clock) once the stores are issued
+            __builtin_amdgcn_s_waitcnt(0);
+            bbacc[0] += __builtin_amdgcn_s_memtime() - t_load;
+            bbacc[5] += 1;
+        }
+#endif
         T best;
         int bu;
-        tdoa_bb::solve_wave<T, TWC, JT>(kp, Wl, M8, tiles, rng, lane, best, bu);
+        tdoa_bb::solve_wave<T, TWC, JT>(kp, Wl, M8, tiles, rng, lane, best, bu, bbacc);
         if (lane == 0) {
             const int ui = (bu < 0 || bu >= kp.U) ? 0 : bu;  // every L compared false: tuple 0
             const int cell = kp.tuple_cell[ui];
@@ -223,6 +239,14 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
             }
         }
     }
+#ifdef TDOA_DIAG
+    {
+        const int gw = blockIdx.x * NW + wave;
+        if (lane == 0 && gw < 8192)
+            for (int i = 0; i < 8; i++)
+                g_diag_bb[gw * 8 + i] = bbacc[i];
+    }
+#endif
 }
 
 int g_grid_bb = -1;  // TDOA_GRID_BB=0: k_grid only (A/B)
@@ -400,3 +424,15 @@ int tdoa_launch_grid(const tdoa_kparams &kp, const tdoa_kout &out, const void *w
     return is_float ? launch<float>(kp, out, (const float *)weighted, B, stream)
                     : launch<int64_t>(kp, out, (const int64_t *)weighted, B, stream);
 }
+
+#ifdef TDOA_DIAG
+extern "C" int tdoa_diag_fetch_bb(unsigned long long *host, int n)
+{
+    if (n > 8192 * 8)
+        n = 8192 * 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_bb), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif

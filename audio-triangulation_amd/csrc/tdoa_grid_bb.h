@@ -26,6 +26,28 @@
 
 namespace tdoa_bb {
 
+// diagnostic build only (TDOA_DIAG): s_memtime cycles per phase accumulated
+// per wave -- [1] bounds, [2] seed reduction + seed evaluation, [3] the other
+// evaluations, [4] evaluation count (k_grid_bb adds [0] frame loads, [5] frames)
+#ifdef TDOA_DIAG
+#define BB_T0() unsigned long long bb_t_ = __builtin_amdgcn_s_memtime()
+#define BB_MARK(k)                                                 \
+    do {                                                           \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+        bbacc[k] += n_ - bb_t_;                                    \
+        bb_t_ = n_;                                                \
+    } while (0)
+#define BB_COUNT(k) (bbacc[k] += 1)
+#else
+#define BB_T0() \
+    do {        \
+    } while (0)
+#define BB_MARK(k) \
+    do {           \
+    } while (0)
+#define BB_COUNT(k) ((void)0)
+#endif
+
 template <typename T> __device__ __forceinline__ T lowest();
 template <> __device__ __forceinline__ int64_t lowest<int64_t>() { return INT64_MIN; }
 template <> __device__ __forceinline__ float lowest<float>() { return -INFINITY; }
@@ -102,8 +124,10 @@ __device__ __forceinline__ void wave_best(T &v, int &i)
 template <typename T, int TWC, int JT>
 __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, T *M8,
                                            const int32_t *tiles, const uint16_t *rng, int lane,
-                                           T &best_out, int &bu_out)
+                                           T &best_out, int &bu_out, unsigned long long (&bbacc)[8])
 {
+    (void)bbacc;
+    BB_T0();
     const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW;
     const T low = lowest<T>();
     // entry bounds, lane-strided, in L's own pair order
@@ -157,6 +181,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             }
         }
     }
+    BB_MARK(1);
     // seed: the entry of largest bound (first on ties; NaN bounds never win)
     T sv = low;
     int st = 0;
@@ -174,6 +199,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
     // evaluate one entry: one tuple per lane; only L > lowest is recorded (the
     // exhaustive scan never records an L equal to its start value)
     auto eval = [&](int t) {
+        BB_COUNT(4);
         const int start = tiles[2 * t], cnt = tiles[2 * t + 1];
         T L = low;
         int ui = INT_MAX;
@@ -205,6 +231,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
     };
     if (NT > 0)
         eval(seed);
+    BB_MARK(2);
 #pragma unroll
     for (int j = 0; j < JT; j++) {
         const int t = lane + 64 * j;
@@ -216,6 +243,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
                 eval(l + 64 * j);
         }
     }
+    BB_MARK(3);
     best_out = best;
     bu_out = bu;
 }
