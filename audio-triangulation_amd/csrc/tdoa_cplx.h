@@ -15,36 +15,25 @@
 
 namespace {
 
-#ifdef TDOA_NO_ASM
-// plain-C forms of the same primitives (the compiler schedules and pads them)
-__device__ __forceinline__ f2 c_addconj(f2 a, f2 b) { return f2{a.x + b.x, a.y - b.y}; }
-__device__ __forceinline__ f2 c_subconj(f2 a, f2 b) { return f2{a.x - b.x, a.y + b.y}; }
-__device__ __forceinline__ f2 c_add_mi(f2 a, f2 b) { return f2{a.x + b.y, a.y - b.x}; }
-__device__ __forceinline__ f2 c_add_i(f2 a, f2 b) { return f2{a.x - b.y, a.y + b.x}; }
-__device__ __forceinline__ f2 c_sub_mi(f2 a, f2 b) { return f2{a.y - b.y, b.x - a.x}; }
-__device__ __forceinline__ f2 c_sub_i(f2 a, f2 b) { return f2{b.y - a.y, a.x - b.x}; }
-__device__ __forceinline__ f2 c_conj_add_i(f2 a, f2 b) { return f2{a.x - b.y, -a.y - b.x}; }
-__device__ __forceinline__ f2 c_conj_add_mi(f2 a, f2 b) { return f2{a.x + b.y, b.x - a.y}; }
-__device__ __forceinline__ f2 c_mul(f2 a, f2 w) { return f2{a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x}; }
-__device__ __forceinline__ f2 c_mulconj(f2 a, f2 w) { return f2{a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y}; }
-__device__ __forceinline__ f2 c_conjmul(f2 a, f2 b) { return f2{a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x}; }
-__device__ __forceinline__ f2 c_mul_s(f2 a, f2 w) { return c_mul(a, w); }
-__device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w) { return c_mulconj(a, w); }
-__device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w) { const f2 r = c_mul(a, w); return f2{-r.x, -r.y}; }
-__device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w) { const f2 r = c_mulconj(a, w); return f2{-r.x, -r.y}; }
-__device__ __forceinline__ f2 c_mi(f2 x) { return f2{x.y, -x.x}; }
-__device__ __forceinline__ f2 c_i(f2 x) { return f2{-x.y, x.x}; }
-__device__ __forceinline__ f2 c_unit(f2 x, float e2)
-{
-    const float r = __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
-    return f2{x.x * r, x.y * r};
-}
-
+#ifdef TDOA_ASM_MUL_S
+// products by compile-time twiddles in an SGPR pair as pinned asm pairs
+// (tdoa_phat_r16.hip, whose scheduling measured better with them)
+#define TDOA_PK_MUL_S(name, mods1, mods2)                                                  \
+    __device__ __forceinline__ f2 name(f2 a, f2 w)                                         \
+    {                                                                                      \
+        f2 t, r;                                                                           \
+        asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]" mods1 "\n\t"                         \
+            "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1]" mods2             \
+            : "=v"(r), "=&v"(t)                                                            \
+            : "v"(a), "s"(w));                                                             \
+        return r;                                                                          \
+    }
+TDOA_PK_MUL_S(c_mul_s, "", " neg_lo:[0,1,0]")
+TDOA_PK_MUL_S(c_mulconj_s, "", " neg_hi:[0,0,1]")
+TDOA_PK_MUL_S(c_negmul_s, " neg_lo:[0,1] neg_hi:[0,1]", " neg_hi:[0,1,0]")
+TDOA_PK_MUL_S(c_negmulconj_s, " neg_lo:[0,1] neg_hi:[0,1]", " neg_lo:[0,1,0] neg_hi:[0,1,1]")
+#undef TDOA_PK_MUL_S
 #else
-#ifndef TDOA_ASM_MUL_S
-#define TDOA_VEC_MUL_S 1
-#endif
-#ifdef TDOA_VEC_MUL_S
 // products by compile-time twiddles (SGPR-pair constants) as plain packed-vector
 // code: splats become op_sel, so each is still v_pk_mul + v_pk_fma, but the
 // post-RA scheduler sees them and fills the packed-result hazard slots
@@ -55,34 +44,8 @@ __device__ __forceinline__ f2 c_mul_s(f2 a, f2 w) { return v_fma(v_yy(a), f2{-w.
 __device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w) { return v_fma(v_yy(a), f2{w.y, w.x}, v_xx(a) * f2{w.x, -w.y}); }
 __device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w) { return c_mul_s(a, f2{-w.x, -w.y}); }
 __device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w) { return c_mulconj_s(a, f2{-w.x, -w.y}); }
-#define TDOA_HAVE_MUL_S 1
 #endif
-#ifdef TDOA_VEC_MUL
-// products as plain packed-vector code (lane splats become op_sel, constants
-// SGPR pairs): the scheduler sees their latencies and hazards and interleaves
-// independent work instead of padding asm blocks with s_nop
-__device__ __forceinline__ f2 v_xx(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
-__device__ __forceinline__ f2 v_yy(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
-__device__ __forceinline__ f2 v_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 c_mul(f2 a, f2 w) { return v_fma(v_yy(a), f2{-w.y, w.x}, v_xx(a) * w); }
-__device__ __forceinline__ f2 c_mulconj(f2 a, f2 w) { return v_fma(v_yy(a), f2{w.y, w.x}, v_xx(a) * f2{w.x, -w.y}); }
-__device__ __forceinline__ f2 c_conjmul(f2 a, f2 b) { return v_fma(v_yy(a), f2{b.y, -b.x}, v_xx(a) * b); }
-__device__ __forceinline__ f2 c_mul_s(f2 a, f2 w) { return c_mul(a, w); }
-__device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w) { return c_mulconj(a, w); }
-__device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w) { return c_mul(a, f2{-w.x, -w.y}); }
-__device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w) { return c_mulconj(a, f2{-w.x, -w.y}); }
-#define TDOA_HAVE_MUL 1
-#endif
-#ifdef TDOA_VEC_ADD
-// single-instruction adds as v_pk_fma by SGPR-pair sign constants (op_sel
-// swaps for the +-i forms), visible to the scheduler
-__device__ __forceinline__ f2 v_sw(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
-__device__ __forceinline__ f2 c_addconj(f2 a, f2 b) { return __builtin_elementwise_fma(b, f2{1.0f, -1.0f}, a); }
-__device__ __forceinline__ f2 c_subconj(f2 a, f2 b) { return __builtin_elementwise_fma(b, f2{-1.0f, 1.0f}, a); }
-__device__ __forceinline__ f2 c_add_mi(f2 a, f2 b) { return __builtin_elementwise_fma(v_sw(b), f2{1.0f, -1.0f}, a); }
-__device__ __forceinline__ f2 c_add_i(f2 a, f2 b) { return __builtin_elementwise_fma(v_sw(b), f2{-1.0f, 1.0f}, a); }
-#define TDOA_HAVE_VEC_ADD 1
-#endif
+
 #define TDOA_PK(name, mnemonic, mods)                                      \
     __device__ __forceinline__ f2 name(f2 a, f2 b)                         \
     {                                                                      \
@@ -90,14 +53,12 @@ __device__ __forceinline__ f2 c_add_i(f2 a, f2 b) { return __builtin_elementwise
         asm(mnemonic " %0, %1, %2 " mods : "=v"(r) : "v"(a), "v"(b));      \
         return r;                                                          \
     }
-#ifndef TDOA_HAVE_VEC_ADD
 // a + conj(b), a - conj(b)
 TDOA_PK(c_addconj, "v_pk_add_f32", "neg_hi:[0,1]")
 TDOA_PK(c_subconj, "v_pk_add_f32", "neg_lo:[0,1]")
 // a - i b = (a.x + b.y, a.y - b.x);  a + i b = (a.x - b.y, a.y + b.x)
 TDOA_PK(c_add_mi, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]")
 TDOA_PK(c_add_i, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]")
-#endif
 // -i (a - b) = (a.y - b.y, b.x - a.x);  i (a - b) = (b.y - a.y, a.x - b.x)
 TDOA_PK(c_sub_mi, "v_pk_add_f32", "op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]")
 TDOA_PK(c_sub_i, "v_pk_add_f32", "op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]")
@@ -106,7 +67,6 @@ TDOA_PK(c_conj_add_i, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]
 TDOA_PK(c_conj_add_mi, "v_pk_add_f32", "op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[1,0]")
 #undef TDOA_PK
 
-#ifndef TDOA_HAVE_MUL
 // a * w
 __device__ __forceinline__ f2 c_mul(f2 a, f2 w)
 {
@@ -137,48 +97,6 @@ __device__ __forceinline__ f2 c_conjmul(f2 a, f2 b)
         : "v"(a), "v"(b));
     return r;
 }
-#ifndef TDOA_HAVE_MUL_S
-// the same with the twiddle in an SGPR pair (compile-time constants)
-__device__ __forceinline__ f2 c_mul_s(f2 a, f2 w)
-{
-    f2 t, r;
-    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
-        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r), "=&v"(t)
-        : "v"(a), "s"(w));
-    return r;
-}
-__device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w)
-{
-    f2 t, r;
-    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
-        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
-        : "=v"(r), "=&v"(t)
-        : "v"(a), "s"(w));
-    return r;
-}
-
-// -(a * w), -(a * conj(w))  (negated twiddle products, SGPR twiddle)
-__device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w)
-{
-    f2 t, r;
-    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-        : "=v"(r), "=&v"(t)
-        : "v"(a), "s"(w));
-    return r;
-}
-__device__ __forceinline__ f2 c_negmulconj_s(f2 a, f2 w)
-{
-    f2 t, r;
-    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,1]"
-        : "=v"(r), "=&v"(t)
-        : "v"(a), "s"(w));
-    return r;
-}
-#endif  // TDOA_HAVE_MUL_S
-#endif  // TDOA_HAVE_MUL
 // -i x = (x.y, -x.x);  i x = (-x.y, x.x)
 __device__ __forceinline__ f2 c_mi(f2 x)
 {
@@ -206,12 +124,6 @@ __device__ __forceinline__ f2 c_unit(f2 x, float e2)
     // whose high dword op_sel_hi ignores (no copy to build {r, r}).  The
     // multiply opens with s_nop 0: a transcendental result read by the next
     // VALU needs one wait state, and the compiler does not pad ahead of asm
-#ifdef TDOA_OLD_UNIT
-    const float r = __builtin_amdgcn_rsqf(fmaxf(s.x, e2));
-    f2 y;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(f2{r, r}));
-    return y;
-#else
     float m;
     asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(s.x), "v"(e2));
     f2 rr;
@@ -219,10 +131,7 @@ __device__ __forceinline__ f2 c_unit(f2 x, float e2)
     f2 y;
     asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(rr));
     return y;
-#endif
 }
-
-#endif  // TDOA_NO_ASM
 
 // W_32^k = e^{-2 pi i k / 32}, k = 1..7 (the others by symmetry)
 __device__ __forceinline__ f2 w32c(int k)

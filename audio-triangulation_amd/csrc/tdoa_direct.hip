@@ -647,20 +647,26 @@ static void direct_geometry(tdoa_kparams &kp, int &threads)
         threads = 1024;
 }
 
-static int direct_use_mfma()
+// workgroup shape of k_direct_mfma: F frames per workgroup (one wave per
+// (frame, pair) up to 16 waves) and the 16-B staging chunks per thread
+static void mf_shape(const tdoa_kparams &kp, int &F, int &threads, int &chunks)
 {
-    // matrix-core path (k_direct_mfma): TDOA_DIRECT_MFMA=0 keeps the VALU kernel (A/B)
-    static const int v = [] {
-        const char *s = getenv("TDOA_DIRECT_MFMA");
-        return s ? atoi(s) : 1;
-    }();
-    return v;
+    F = kp.P >= 16 ? 1 : 16 / kp.P > 4 ? 4 : 16 / kp.P;
+    threads = 64 * (F * kp.P < 16 ? F * kp.P : 16);
+    chunks = (F * kp.M * kp.N / 8 + threads - 1) / threads;
 }
 
-// the matrix-core kernel (config 2..4 shapes) runs the grid solve itself
+// the matrix-core kernel (config 2..4 shapes) runs the grid solve itself; a
+// shape whose frames exceed its staging registers (e.g. 2 mics x 4096: one
+// wave per frame holds 16 chunks per thread) takes the VALU k_direct and the
+// separate grid launch
 bool tdoa_direct_fused_grid(const tdoa_kparams &kp)
 {
-    return direct_use_mfma() && kp.N % 64 == 0 && kp.N >= 64 && kp.S <= 63;
+    if (!(kp.N % 64 == 0 && kp.N >= 64 && kp.S <= 63))
+        return false;
+    int F, threads, chunks;
+    mf_shape(kp, F, threads, chunks);
+    return chunks <= 8;
 }
 
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
@@ -675,8 +681,8 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         const int n0 = (kp.S + 15) / 16, nq = n0 + (kp.S + 1 + 15) / 16;  // lag columns -16 n0 .. 16 (nq - n0) - 1
         kp.PADW = MF_PADW;
         kp.RS = kp.N / 2 + 2 * MF_PADW;
-        kp.F = kp.P >= 16 ? 1 : 16 / kp.P > 4 ? 4 : 16 / kp.P;  // frames per workgroup: one wave per (frame, pair) up to 16
-        threads = 64 * (kp.F * kp.P < 16 ? kp.F * kp.P : 16);
+        int chunks = 0;
+        mf_shape(kp, kp.F, threads, chunks);
         MfTabs tb;
         size_t o = smem_bytes(kp, threads / 64);
         tb.rsum = (int)o;
@@ -698,9 +704,6 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         const int64_t grid = (B + kp.F - 1) / kp.F;
         if (grid > INT_MAX)
             return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
-        const int chunks = (kp.F * kp.M * kp.N / 8 + threads - 1) / threads;  // per thread
-        if (chunks > 8)
-            return tdoa_set_error(-1, "DIRECT: frames too large for the staging registers");
         hipStream_t st = (hipStream_t)stream;
         constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
 #define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                  \

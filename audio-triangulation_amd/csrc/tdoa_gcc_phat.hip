@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
             buf[swz(2 * c, lane)] = cmulf(v[brev5(2 * c)], f2{q.x, q.y});
             buf[swz(2 * c + 1, lane)] = cmulf(v[brev5(2 * c + 1)], f2{q.z, q.w});
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
 #pragma unroll
         for (int c = 0; c < 16; c++) {
             const float4 q = *reinterpret_cast<const float4 *>(&buf[swz(lane, 2 * c)]);
@@ -495,7 +495,7 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
             v[2 * c + 1] = f2{q.z, q.w};
         }
         fft32<false, false>(v);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         // spectrum Z[lane + 32 k] at (row k, col lane)
 #pragma unroll
         for (int k = 0; k < 32; k++)
@@ -567,14 +567,14 @@ __global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_
         for (int k1 = 0; k1 < 32; k1++)
             v[k1] = buf[swz(k1, lane)];
         fft32<true, false>(v);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
 #pragma unroll
         for (int c = 0; c < 16; c++) {
             const float4 q = *reinterpret_cast<const float4 *>(&twm[swz(lane, 2 * c)]);
             buf[swz(2 * c, lane)] = cmulf(v[brev5(2 * c)], f2{q.x, -q.y});
             buf[swz(2 * c + 1, lane)] = cmulf(v[brev5(2 * c + 1)], f2{q.z, -q.w});
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
 #pragma unroll
         for (int c = 0; c < 16; c++) {
             const float4 q = *reinterpret_cast<const float4 *>(&buf[swz(lane, 2 * c)]);
@@ -692,12 +692,8 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (tdoa_phat1024_fits(kp))
         return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
     // frame_len 2048 / 4096 with M > 3 or N > 2048: register-pass kernels
-    // (tdoa_phat_r16.hip); TDOA_PHAT_R16=0 keeps the LDS Stockham pair (A/B)
-    static const int use_r16 = [] {
-        const char *s = getenv("TDOA_PHAT_R16");
-        return s ? atoi(s) : 1;
-    }();
-    if (tdoa_gcc_phat_needs_split(kp.M, kp.N) && use_r16 && tdoa_phat_r16_fits(kp.M, kp.N, kp.S))
+    // (tdoa_phat_r16.hip); other long shapes the LDS Stockham pair
+    if (tdoa_gcc_phat_needs_split(kp.M, kp.N) && tdoa_phat_r16_fits(kp.M, kp.N, kp.S))
         return tdoa_launch_phat_r16(kp, out, frames, B, phat_eps, spec_scratch, spec_bytes, stream);
     if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
         return tdoa_launch_gcc_phat_split(kp, out, frames, B,

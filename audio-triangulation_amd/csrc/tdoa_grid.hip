@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 #ifdef TDOA_DIAG
         const unsigned long long t_load = __builtin_amdgcn_s_memtime();
 #endif
-        __builtin_amdgcn_wave_barrier();  // the previous frame's reads of Wl come first
+        wave_lds_sync();  // the previous frame's reads of Wl come first
         {
             // the frame's P x K scores (10.4 KB at config 4): 16-B loads, eight per
             // lane in flight before their LDS stores (one element per load and
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
             for (int e = e0 + lane; e < PK; e += 64)
                 Wl[e] = src[e];
         }
-        __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+        wave_lds_sync();  // a wave's LDS operations complete in order
 #ifdef TDOA_DIAG
         {
             // the loads' data reaches LDS (and so the clock) once the stores are issued
@@ -249,7 +249,6 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 #endif
 }
 
-int g_grid_bb = -1;  // TDOA_GRID_BB=0: k_grid only (A/B)
 
 template <typename T, int TWC, int JT>
 int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
@@ -287,11 +286,7 @@ int launch_bb_jt(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted
 template <typename T>
 bool bb_fits(const tdoa_kparams &kp)
 {
-    if (g_grid_bb < 0) {
-        const char *s = getenv("TDOA_GRID_BB");
-        g_grid_bb = s ? atoi(s) : 1;
-    }
-    if (!g_grid_bb || kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
+    if (kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
         return false;
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
     return kp.K <= 127 && table + ((size_t)kp.P * kp.K + 128) * sizeof(T) <= 150 * 1024;

@@ -158,7 +158,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
         // M8[max(lo, hi - 7)]) -- independent reads, not a dependent chain
         for (int p = 0; p < P; p++) {
             const T *w = Wl + p * K;
-            __builtin_amdgcn_wave_barrier();  // previous pair's M8 reads come first
+            wave_lds_sync();  // previous pair's M8 reads come first
             for (int k = lane; k < K; k += 64) {
                 T m = w[k];
 #pragma unroll
@@ -166,7 +166,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
                     m = vmax<T>(m, w[k + d < K ? k + d : K - 1]);
                 M8[k] = m;
             }
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
 #pragma unroll
             for (int j = 0; j < JT; j++) {
                 const int t = lane + 64 * j;

@@ -7,6 +7,22 @@
 
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
+// Lanes of one wave exchanging data through LDS (transpose tiles, score
+// tables, staging rows): the wave's DS instructions execute in issue order,
+// but the compiler models each lane as a thread of its own and may move one
+// lane's LDS write past a later read it cannot prove disjoint.  The wavefront-
+// scope release/acquire fences order the memory operations at the IR level
+// (they emit no instruction for LDS); the wave barrier between them keeps the
+// lanes together (rocPRIM's wave-sync pattern).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 #define TDOA_MAX_PAIRS 28  // 8 mics
 #define TDOA_MAX_MICS_K 8
 #define TDOA_LS_ITERS 10   // least-squares refinement steps (tdoa_ls.hip)
@@ -127,10 +143,9 @@ int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
                    const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
                    int64_t B, void *stream);
 size_t tdoa_stream_trigger_lds(int M, int N, int H);
-// the trigger launch for this stream writes each triggered frame at its
-// stream's index (k_stream_trigger_p) instead of its compact slot
-bool tdoa_stream_trigger_by_id(const tdoa_stream_params &sp, int64_t S);
-int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream);
+// *by_id: the launch wrote each triggered frame at its stream's index
+// (k_stream_trigger_p) instead of its compact slot -- the layout DIRECT reads
+int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream, bool *by_id);
 int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &kp,
                               const tdoa_stream_kout &out, int64_t S, void *stream);
 int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est,

@@ -50,8 +50,7 @@ namespace {
 constexpr int P1K_ROW = 264;              // tile row stride, bytes (32 complex + 8 B pad)
 constexpr int P1K_TILE = 32 * P1K_ROW;    // 8448 B: one transpose of one half-wave
 constexpr int P1K_KPAD = 128;             // lag slots per pair in the grid score table
-template <bool DUAL>
-constexpr int p1k_wave_lds() { return (DUAL ? 4 : 2) * P1K_TILE; }  // tiles per wave
+constexpr int P1K_WAVE_LDS = 2 * P1K_TILE;  // a wave's two transpose tiles (one per half-wave)
 constexpr int P1K_GB = 8;                 // grid tuples per lane per batch
 // LDS table image: twm [32][32] f2 | tw2 [16][32] f2 | win [512] f2 | prior [128] | tuples
 constexpr int P1K_IMG_FIXED = 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4;
@@ -145,14 +144,6 @@ __device__ __forceinline__ void swap_upper_exec(f2 (&V)[NV], f2 E)
         V[16 + j] = y[j];
 }
 
-__device__ __forceinline__ void better(float &bv, int &bu, float ov, int ou)
-{
-    if (ov > bv || (ov == bv && ou < bu)) {
-        bv = ov;
-        bu = ou;
-    }
-}
-
 // sum over the 32 lanes of each half-wave, VALU only (no LDS queue): row
 // all-reduce by DPP, row_bcast:15 into rows 1 and 3, then lanes 31 / 63
 __device__ __forceinline__ int hsum32(int s, int hw)
@@ -184,12 +175,6 @@ __device__ __forceinline__ f2 unit(f2 x, float e2)
     return x * __builtin_amdgcn_rsqf(fmaxf(x.x * x.x + x.y * x.y, e2));
 }
 
-// Lanes of a wave exchange data through LDS (the transposes, the grid score
-// table): a wave's DS instructions execute in issue order, but the compiler
-// models each lane as a separate thread and may reorder one lane's LDS write
-// and a later read it cannot prove aliasing.  This compiler-only barrier
-// (no instruction) pins the order of the wave's memory operations.
-__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_wave_barrier(); }
 
 struct Lane {
     int hw;           // half-wave of the wave
@@ -197,56 +182,11 @@ struct Lane {
     int res;          // residue column
     int cs;           // its tile / table slot, slot(res)
     bool is0, is1;    // the self-paired lanes
-    char *tileA;      // this half-wave's two transpose tiles
-    char *tileB;
+    char *tileA;      // this half-wave's transpose tile
     const char *twm;  // [k][r] W_1024^{r k}
     const char *tw2;  // [k][r] W_2048^{r + 32 k}, k < 16
     const char *win;  // [w] (W[2w], W[2w+1]) / 128
 };
-
-// per-lane table values, read into registers at the start of a phase (before
-// its tile writes, which the compiler cannot prove disjoint from the tables)
-__device__ __forceinline__ void load_twm(const Lane &L, f2 (&tw)[32])  // W_1024^{res k}
-{
-#pragma unroll
-    for (int k = 1; k < 32; k++)
-        tw[k] = lds_f2(L.twm, 8 * L.cs + 256 * k);
-}
-__device__ __forceinline__ void load_tw2(const Lane &L, f2 (&t2)[16])  // W_2048^{res + 32 k}
-{
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-        t2[k] = lds_f2(L.tw2, 8 * L.cs + 256 * k);
-}
-__device__ __forceinline__ void load_win(const Lane &L, f2 (&wf)[16])  // W / 128 of words res + 32 t
-{
-#pragma unroll
-    for (int t = 0; t < 16; t++)
-        wf[t] = lds_f2(L.win, 8 * L.cs + 256 * t);
-}
-
-// integer front end of one mic row (16 words per lane) -> v[t] = z[res + 32 t]
-__device__ __forceinline__ void front_end(const Lane &L, const uint32_t (&w)[16], f2 (&v)[32],
-                                          const f2 (&wfa)[16])
-{
-    int s = 0;
-#pragma unroll
-    for (int t = 0; t < 16; t++)
-        s = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_t, w[t]), v2s_t{1, 1}, s, false);
-    s = hsum32(s, L.hw);
-    // floor-mean DC (int64 arithmetic shift == floor), low byte of x - off
-    // (x <<= 8 keeps only it), ((s << 8) * W) >> 15 == floor(s * W / 128):
-    // exact in fp32, samples stay in int16 units
-    const uint32_t off = (uint32_t)(s >> 10) & 0xFFu;
-    const uint32_t off2 = off | (off << 16);
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-        const uint32_t d = (w[t] | 0x01000100u) - off2;  // no borrow across the halves
-        const float s0 = (float)(int8_t)(d & 0xFFu);
-        const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
-        v[t] = f2{floorf(s0 * wfa[t].x), floorf(s1 * wfa[t].y)};
-    }
-}
 
 // first half of a 32 x 32 FFT_1024 on a residue column: DFT-32 in registers,
 // twiddle W_1024^{-+res k}, column write into the tile
@@ -256,7 +196,7 @@ template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *tile)
 {
     fft32p<INV, HALF_ZERO>(v);
-    wave_lds_order();  // after the previous pass's row reads of this tile
+    wave_lds_sync();  // after the previous pass's row reads of this tile
     const int wo = 8 * L.cs;
 #pragma unroll
     for (int k0 = 0; k0 < 32; k0 += 8) {
@@ -273,22 +213,7 @@ __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *ti
             sts_f2(tile, wo + P1K_ROW * slot(k), x);
         }
     }
-    wave_lds_order();  // before the row reads of other lanes' columns
-}
-template <bool INV, bool HALF_ZERO>
-__device__ __forceinline__ void fft_col(const Lane &L, f2 (&v)[32], char *tile, const f2 (&tw)[32])
-{
-    fft32p<INV, HALF_ZERO>(v);
-    wave_lds_order();
-    const int wo = 8 * L.cs;
-#pragma unroll
-    for (int k = 0; k < 32; k++) {
-        f2 x = v[brev5(k)];
-        if (k)
-            x = INV ? c_mulconj(x, tw[k]) : c_mul(x, tw[k]);
-        sts_f2(tile, wo + P1K_ROW * slot(k), x);
-    }
-    wave_lds_order();
+    wave_lds_sync();  // before the row reads of other lanes' columns
 }
 // second half: row read (row res) + forward DFT-32 -> V[k2] = Z[res + 32 k2]
 __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 (&V)[33])
@@ -303,460 +228,12 @@ __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 
     for (int k = 0; k < 32; k++)
         V[k] = v[brev5(k)];
 }
-// second half of the inverse, pruned: y[res] (y0) and y[res + 992] (y31)
-__device__ __forceinline__ void fft_row_inv(const Lane &L, const char *tile, f2 &y0, f2 &y31)
-{
-    f2 v[32];
-    const int ro = P1K_ROW * L.cs;
-#pragma unroll
-    for (int n = 0; n < 32; n++)
-        v[n] = lds_f2(tile, ro + 8 * slot(n));
-    // outputs n2 = 0 and 31 of the second DFT-32: y0 = sum v[r],
-    // y31 = sum v[r] W_32^r = sum_{r<16} (v[r] - v[r+16]) W_32^r
-    f2 a[16], d[16];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        a[r] = v[r] + v[r + 16];
-        d[r] = tw_only<false>(v[r] - v[r + 16], r);
-    }
-#pragma unroll
-    for (int h = 8; h >= 1; h >>= 1)
-#pragma unroll
-        for (int r = 0; r < h; r++) {
-            a[r] = a[r] + a[r + h];
-            d[r] = d[r] + d[r + h];
-        }
-    y0 = a[0];
-    y31 = d[0];
-}
-
-// real-FFT split + per-bin unit normalisation, in place: residue column ->
-// paired layout (V[k], V[31-k] hold bins b, N-b; V[32] = bin 512 on lane 0)
-__device__ __forceinline__ void split_unit(const Lane &L, f2 (&V)[33], float e2, const f2 (&t2)[16])
-{
-    V[32] = c_unit(conjf2(V[16]), e2);  // X[512] = conj(Z[512]) (x2), lane 0
-#pragma unroll
-    for (int j = 16; j < 32; j++) {  // ascending: lane 0 reads V[j+1] before it changes
-        const f2 t = dpp_xor1(V[j]);
-        const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
-        V[j] = (L.is0 || L.is1) ? own : t;
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const f2 A = V[k], Bv = V[31 - k];
-        const f2 w = t2[k];  // W_2048^b
-        const f2 e = c_addconj(A, Bv);
-        const f2 od = c_mul(c_subconj(A, Bv), w);
-        // X[b] = e - i W^b d,  X[N-b] = conj(e + i W^b d)   (both x2; PHAT is scale-free)
-        V[k] = c_unit(c_add_mi(e, od), e2);
-        V[31 - k] = c_unit(c_conj_add_i(e, od), e2);
-    }
-}
-
-// U <- conj(U) V  (unit cross spectrum R_ij = conj(U_i) U_j, paired layout incl. slot 32)
-__device__ __forceinline__ void cross(f2 (&U)[33], const f2 (&V)[33])
-{
-#pragma unroll
-    for (int k = 0; k < 33; k++)
-        U[k] = c_conjmul(U[k], V[k]);
-}
-
-// packed inverse input Y from the cross spectrum R (paired layout), in place,
-// then back to residue columns
-__device__ __forceinline__ void pretwiddle(const Lane &L, f2 (&V)[33], const f2 (&t2)[16])
-{
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const f2 Rk = V[k], Rn = V[31 - k];
-        const f2 w = t2[k];
-        const f2 s = c_addconj(Rk, Rn);
-        const f2 q = c_mulconj(c_subconj(Rk, Rn), w);
-        V[k] = c_add_i(s, q);              // s + i q
-        V[31 - k] = c_conj_add_mi(s, q);   // conj(s - i q)
-    }
-    const f2 Ye = f2{2.0f * V[32].x, -2.0f * V[32].y};  // Y[512] = 2 conj(R[512])
-#pragma unroll
-    for (int j = 31; j >= 16; j--) {  // descending: lane 0 reads V[j-1] before it changes
-        const f2 t = dpp_xor1(V[j]);
-        const f2 own = L.is0 ? (j == 16 ? Ye : V[j - 1]) : V[j];
-        V[j] = (L.is0 || L.is1) ? own : t;
-    }
-}
-
-__device__ __forceinline__ void copy32(f2 (&d)[32], const f2 (&s)[33])
-{
-#pragma unroll
-    for (int k = 0; k < 32; k++)
-        d[k] = s[k];
-}
-
 }  // namespace
 
 #ifdef TDOA_DIAG
-// diagnostic build only: per-wave cycles per phase of k_phat1024
+// diagnostic build only: per-wave phase stamps of k_p1k_lean
 __device__ unsigned long long g_diag_p1k[1 << 16];
-#define P1K_MARK(i)                                                 \
-    do {                                                            \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        ph_acc[i] += t_ - ph_t;                                     \
-        ph_t = t_;                                                  \
-    } while (0)
-#else
-#define P1K_MARK(i) \
-    do {            \
-    } while (0)
 #endif
-
-// NW waves per workgroup, 2 frames per wave (one per half-wave) per iteration.
-// DUAL: two FFT streams per half-wave (two tiles each); else one at a time.
-template <int NW, bool DUAL>
-__global__ void __launch_bounds__(NW * 64) k_phat1024(tdoa_kparams kp, tdoa_kout out,
-                                                      const int16_t *__restrict__ frames,
-                                                      int64_t B, float e2)
-{
-    constexpr int N = 1024, P = 3, NF = 2 * NW, NT = NW * 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int WAVE_LDS = p1k_wave_lds<DUAL>();
-    char *tiles = smem;                         // [NW][WAVE_LDS]
-    char *twm = tiles + NW * WAVE_LDS;          // [32][32] f2
-    char *tw2 = twm + 32 * 32 * 8;              // [16][32] f2
-    char *win = tw2 + 16 * 32 * 8;              // [512] f2
-    float *prior = (float *)(win + 512 * 8);    // [128]
-    uint32_t *tups = (uint32_t *)(prior + 128); // [U] distinct lag tuples (grid), resident
-
-    const int tid = threadIdx.x, wave = tid >> 6, hw = (tid >> 5) & 1, lane64 = tid & 63;
-    Lane L;
-    L.hw = hw;
-    L.lane = tid & 31;
-    L.res = lane_res(L.lane);
-    L.cs = slot(L.res);
-    L.is0 = L.lane == 0;
-    L.is1 = L.lane == 1;
-    char *wtiles = tiles + wave * WAVE_LDS;
-    L.tileA = wtiles + hw * P1K_TILE;
-    L.tileB = DUAL ? wtiles + (2 + hw) * P1K_TILE : L.tileA;
-    L.twm = twm;
-    L.tw2 = tw2;
-    L.win = win;
-
-#ifdef TDOA_DIAG
-    unsigned long long ph_acc[16] = {};
-    unsigned long long ph_t = __builtin_amdgcn_s_memtime();
-#endif
-    const int K = kp.K, S = kp.S;
-    const bool do_grid = out.cell || out.xy || out.max_Lf;
-    const int Upad = (kp.U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
-
-    // frame words of this half-wave's frame (issued before the table staging so
-    // the first HBM round trip overlaps it), the next iteration's prefetched
-    uint32_t w0[16], w1[16], w2[16], n0[16], n1[16], n2[16];
-    // unconditional loads (a frame past the batch re-reads the last one and
-    // stores nothing): a per-load select would serialise the loads on vmcnt
-    auto fetch = [&](uint32_t(&w)[16], int64_t fr, int m) {
-        const uint32_t *row = reinterpret_cast<const uint32_t *>(
-            frames + ((fr < B ? fr : B - 1) * 3 + m) * (int64_t)N) + L.res;
-#pragma unroll
-        for (int t = 0; t < 16; t++)
-            w[t] = __builtin_nontemporal_load(row + 32 * t);
-    };
-    if constexpr (DUAL) {
-        const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
-        fetch(n0, f, 0);
-        fetch(n1, f, 1);
-        fetch(n2, f, 2);
-    }
-
-    // host-built table image (tdoa_phat1024_image): twm | tw2 | win | prior | tuples
-    {
-        const uint4 *src = (const uint4 *)kp.p1k_img;
-        uint4 *dst = (uint4 *)twm;
-        const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
-#pragma unroll 8
-        for (int e = tid; e < n16; e += NT)
-            dst[e] = src[e];
-    }
-    __syncthreads();
-    P1K_MARK(0);
-
-    const float invL = 1.0f / 2048.0f;
-    // this lane's four candidate lags: y[res+992] -> 2 res - 64 (+1), y[res] -> 2 res (+1),
-    // in ascending lag order (first max wins, correlations.c:20-23)
-    const int la = 2 * L.res, lb = 2 * L.res - 64;
-    const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
-    const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
-
-    // weighted scores of the previous iteration's frames, held for a grid pass
-    // over four frames (two iterations) at once
-    float pv[3][4];
-    int64_t pbase = -1;
-    const int64_t stride = (int64_t)gridDim.x * NF;
-    for (int64_t base = (int64_t)blockIdx.x * NF; base < B; base += stride) {
-        const int64_t f = base + 2 * wave + hw;
-        const bool live = f < B;
-        const int64_t fn = f + (int64_t)gridDim.x * NF;  // next iteration's frame
-        if constexpr (DUAL) {
-#pragma unroll
-            for (int t = 0; t < 16; t++) {
-                w0[t] = n0[t];
-                w1[t] = n1[t];
-                w2[t] = n2[t];
-            }
-            // the next frame's words are fetched after the register peak of
-            // this iteration (pair (0,1) inverse | mic 2 forward), not here
-        } else {  // two waves per SIMD cover the load latency: one mic ahead only
-            fetch(w0, f, 0);
-            fetch(w1, f, 1);
-        }
-#ifdef TDOA_DIAG
-        ph_acc[15]++;
-#endif
-
-        float wv[3][4];
-        int best[3];
-        // argmax + prior + outputs of pair p from y[res] (y0) and y[res+992] (y31)
-        auto finish_pair = [&](int p, f2 y0, f2 y31) {
-            const float cv[4] = {y31.x * invL, y31.y * invL, y0.x * invL, y0.y * invL};
-            float bv = -INFINITY;
-            int bk = INT_MAX;
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-                if (ok[c] && (cv[c] > bv || bk == INT_MAX)) {
-                    bv = cv[c];
-                    bk = ck[c];
-                }
-            half_argmax_to31(bv, bk);
-            const int b0 = __builtin_amdgcn_readlane(bk, 31), b1 = __builtin_amdgcn_readlane(bk, 63);
-            bk = hw ? b1 : b0;  // uniform per half-wave even for NaN scores
-            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
-            best[p] = bk - S;
-            const size_t gb = (size_t)(f * P + p) * K;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int d = ck[c] > bk ? ck[c] - bk : bk - ck[c];
-                wv[p][c] = ok[c] ? cv[c] * prior[ok[c] ? d : 0] : 0.0f;
-                if (live && ok[c]) {
-                    if (out.scores_f)
-                        out.scores_f[gb + ck[c]] = cv[c];
-                    if (out.weighted_f)
-                        out.weighted_f[gb + ck[c]] = wv[p][c];
-                }
-            }
-            if (live && L.lane == 0)
-                out.lags[f * P + p] = bk - S;
-        };
-
-        f2 U0[33], U1[33], V[33], va[32], vb[32], y0, y31, z0, z31;
-        f2 tw[32], t2[16], wf[16];
-        if constexpr (DUAL) {
-            // mic 0 | mic 1 forward, split + unit normalisation
-            load_win(L, wf);
-            load_twm(L, tw);
-            front_end(L, w0, va, wf);
-            front_end(L, w1, vb, wf);
-            fft_col<false, true>(L, va, L.tileA, tw);
-            fft_col<false, true>(L, vb, L.tileB, tw);
-            fft_row_fwd(L, L.tileA, U0);
-            fft_row_fwd(L, L.tileB, U1);
-            P1K_MARK(1);
-            load_tw2(L, t2);
-            split_unit(L, U0, e2, t2);
-            split_unit(L, U1, e2, t2);
-            P1K_MARK(2);
-            // pair (0,1) inverse | mic 2 forward
-            load_win(L, wf);
-            load_twm(L, tw);
-#pragma unroll
-            for (int k = 0; k < 33; k++)
-                V[k] = U0[k];
-            cross(V, U1);
-            pretwiddle(L, V, t2);
-            copy32(va, V);
-            front_end(L, w2, vb, wf);
-            fft_col<true, false>(L, va, L.tileA, tw);
-            fft_col<false, true>(L, vb, L.tileB, tw);
-            fft_row_inv(L, L.tileA, y0, y31);
-            fft_row_fwd(L, L.tileB, V);
-            finish_pair(0, y0, y31);
-            fetch(n0, fn, 0);
-            fetch(n1, fn, 1);
-            fetch(n2, fn, 2);
-            P1K_MARK(3);
-            load_tw2(L, t2);
-            split_unit(L, V, e2, t2);
-            cross(U0, V);  // pair 1: (0, 2)
-            cross(U1, V);  // pair 2: (1, 2)
-            P1K_MARK(4);
-            // pair (0,2) | pair (1,2) inverse
-            load_twm(L, tw);
-            pretwiddle(L, U0, t2);
-            pretwiddle(L, U1, t2);
-            copy32(va, U0);
-            copy32(vb, U1);
-            fft_col<true, false>(L, va, L.tileA, tw);
-            fft_col<true, false>(L, vb, L.tileB, tw);
-            fft_row_inv(L, L.tileA, y0, y31);
-            fft_row_inv(L, L.tileB, z0, z31);
-            finish_pair(1, y0, y31);
-            finish_pair(2, z0, z31);
-        } else {
-            // one stream: at most three spectra live (U0, U1, V)
-            load_win(L, wf);
-            front_end(L, w0, va, wf);
-            fetch(w2, f, 2);
-            fft_col_lds<false, true>(L, va, L.tileA);
-            fft_row_fwd(L, L.tileA, U0);
-            load_tw2(L, t2);
-            split_unit(L, U0, e2, t2);
-            load_win(L, wf);
-            front_end(L, w1, va, wf);
-            fft_col_lds<false, true>(L, va, L.tileA);
-            fft_row_fwd(L, L.tileA, U1);
-            load_tw2(L, t2);
-            split_unit(L, U1, e2, t2);
-            P1K_MARK(1);
-#pragma unroll
-            for (int k = 0; k < 33; k++)
-                V[k] = U0[k];
-            cross(V, U1);  // pair 0: (0, 1)
-            load_tw2(L, t2);
-            pretwiddle(L, V, t2);
-            copy32(va, V);
-            fft_col_lds<true, false>(L, va, L.tileA);
-            fft_row_inv(L, L.tileA, y0, y31);
-            finish_pair(0, y0, y31);
-            P1K_MARK(2);
-            load_win(L, wf);
-            front_end(L, w2, va, wf);
-            fft_col_lds<false, true>(L, va, L.tileA);
-            fft_row_fwd(L, L.tileA, V);
-            load_tw2(L, t2);
-            split_unit(L, V, e2, t2);
-            cross(U0, V);  // pair 1: (0, 2)
-            cross(U1, V);  // pair 2: (1, 2)
-            P1K_MARK(3);
-            load_tw2(L, t2);
-            pretwiddle(L, U0, t2);
-            copy32(va, U0);
-            fft_col_lds<true, false>(L, va, L.tileA);
-            fft_row_inv(L, L.tileA, y0, y31);
-            finish_pair(1, y0, y31);
-            P1K_MARK(4);
-            load_tw2(L, t2);
-            pretwiddle(L, U1, t2);
-            copy32(va, U1);
-            fft_col_lds<true, false>(L, va, L.tileA);
-            fft_row_inv(L, L.tileA, z0, z31);
-            finish_pair(2, z0, z31);
-        }
-        if (live && L.lane == 0 && out.gate)
-            out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
-        P1K_MARK(5);
-
-        if (!do_grid)
-            continue;
-        // ---- grid solve (vga_heatmap.h:99-108) once per two iterations: the
-        // weighted scores of this wave's four frames (previous iteration: slots
-        // 0, 1; this one: slots 2, 3) -> [p][k][4] in the wave's tile space, so
-        // one b128 gather per pair reads all four; lanes split the tuples and
-        // keep (max L, first tuple) per frame.  An unpaired iteration (the last
-        // of an odd count) fills slots 0, 1 with its own frames.
-        if (pbase < 0 && base + stride < B) {
-#pragma unroll
-            for (int p = 0; p < P; p++)
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                    pv[p][c] = wv[p][c];
-            pbase = base;
-            continue;
-        }
-        const bool paired = pbase >= 0;
-        wave_lds_order();
-        float *wsc = (float *)wtiles;  // [P][KPAD][4]
-#pragma unroll
-        for (int p = 0; p < P; p++)
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-                if (ok[c]) {
-                    float *d = wsc + (p * P1K_KPAD + ck[c]) * 4;
-                    d[hw] = paired ? pv[p][c] : wv[p][c];
-                    d[2 + hw] = wv[p][c];
-                }
-        if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
-            *(float4 *)(wsc + (L.lane * P1K_KPAD + P1K_KPAD - 1) * 4) =
-                float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        wave_lds_order();
-        float gv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        int gu[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
-        const char *ws = (const char *)wsc;
-        // each lane scores 4 consecutive tuples per step (one b128 read of their
-        // words, 12 b128 gathers: within the 15 LDS operations a wave may have
-        // in flight); the next step's words are read while the gathers land.
-        // Per lane the tuples ascend, so a strict '>' keeps the first maximum.
-        P1K_MARK(7);
-        const uint4 *tq = (const uint4 *)tups;
-        uint4 q = tq[lane64];
-        for (int u0 = 0; u0 < Upad; u0 += 256) {
-            const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
-            float4 Lg[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                // tuple fields are byte offsets of f2 slots: x2 for float4 slots
-                const float4 l0 = *(const float4 *)(ws + 2 * (int)(wq[i] & 0x3FFu));
-                const float4 l1 = *(const float4 *)(ws + P1K_KPAD * 16 + 2 * (int)((wq[i] >> 10) & 0x3FFu));
-                const float4 l2 = *(const float4 *)(ws + 2 * P1K_KPAD * 16 + 2 * (int)(wq[i] >> 20));
-                Lg[i] = (l0 + l1) + l2;
-            }
-            q = tq[(u0 + 256 < Upad ? u0 + 256 : u0) / 4 + lane64];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int u = u0 + 4 * lane64 + i;
-                const float lv[4] = {Lg[i].x, Lg[i].y, Lg[i].z, Lg[i].w};
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (lv[j] > gv[j]) {
-                        gv[j] = lv[j];
-                        gu[j] = u;
-                    }
-            }
-        }
-        P1K_MARK(8);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            wave_argmax_to63(gv[j], gu[j]);
-        P1K_MARK(9);
-        if (lane64 == 63) {
-            // every L compared false (NaN scores): tuple 0
-            int cells[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)  // all loads first
-                cells[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int64_t fs = (j < 2 ? pbase : base) + 2 * wave + (j & 1);
-                const float v = gv[j];
-                const int cell = cells[j];
-                if ((j >= 2 || paired) && fs < B) {
-                    if (out.cell)
-                        out.cell[fs] = cell;
-                    if (out.max_Lf)
-                        out.max_Lf[fs] = v;
-                    if (out.xy) {
-                        const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
-                        out.xy[2 * fs] = (float)(cx - kp.half_w) / kp.grid_scale;
-                        out.xy[2 * fs + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
-                    }
-                }
-            }
-        }
-        pbase = -1;
-        P1K_MARK(6);
-    }
-#ifdef TDOA_DIAG
-    if ((tid & 63) == 0 && (blockIdx.x * NW + wave) < 4096)
-        for (int i = 0; i < 16; i++)
-            g_diag_p1k[(blockIdx.x * NW + wave) * 16 + i] = ph_acc[i];
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // k_p1k_lean: the same per-frame algorithm at TWO waves per SIMD (8 waves per
@@ -804,16 +281,7 @@ __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)
     fft_col_lds<false, true>(L, v, L.tileA);
     fft_row_fwd(L, L.tileA, V);
     V[32] = c_unit(conjf2(V[16]), e2);
-#ifdef P1K_SELECT_SWAP
-#pragma unroll
-    for (int j = 16; j < 32; j++) {
-        const f2 t = dpp_xor1(V[j]);
-        const f2 own = L.is0 ? V[(j + 1) & 31] : V[j];
-        V[j] = (L.is0 || L.is1) ? own : t;
-    }
-#else
     swap_upper_exec<true>(V, f2{0.0f, 0.0f});
-#endif
 }
 
 // real-FFT split of the partner pair k + unit normalisation: the unit
@@ -948,16 +416,7 @@ __device__ __forceinline__ void lean_pretwiddle(const Lane &L, const f2 (&A)[33]
     }
     const f2 R32 = CROSS ? c_conjmul(A[32], Bs[32]) : A[32];
     const f2 Ye = f2{2.0f * R32.x, -2.0f * R32.y};  // Y[512] = 2 conj(R[512])
-#ifdef P1K_SELECT_SWAP
-#pragma unroll
-    for (int j = 31; j >= 16; j--) {
-        const f2 t = dpp_xor1(v[j]);
-        const f2 own = L.is0 ? (j == 16 ? Ye : v[j - 1]) : v[j];
-        v[j] = (L.is0 || L.is1) ? own : t;
-    }
-#else
     swap_upper_exec<false>(v, Ye);
-#endif
 }
 
 }  // namespace
@@ -1023,7 +482,6 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     L.is1 = L.lane == 1;
     char *wtiles = tiles + wave * 2 * P1K_TILE;
     L.tileA = wtiles + hw * P1K_TILE;
-    L.tileB = L.tileA;
     L.twm = twm;
     L.tw2 = tw2;
     L.win = win;
@@ -1039,21 +497,6 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         for (int t = 0; t < 16; t++)
             w[t] = __builtin_nontemporal_load(row + 32 * t);
     };
-#ifdef LEAN_OLD_STAGING
-    uint32_t w0[16], w1[16];
-    {
-        const uint4 *src = (const uint4 *)kp.p1k_img;
-        uint4 *dst = (uint4 *)twm;
-        const int n16 = do_grid ? kp.p1k_img_bytes / 16 : P1K_IMG_FIXED / 16;
-        for (int e = tid; e < n16; e += NT)
-            dst[e] = src[e];
-    }
-    __syncthreads();
-    {
-        const int64_t f = (int64_t)blockIdx.x * NF + 2 * wave + hw;
-        fetch(w0, f, 0);
-    }
-#else
     // table image: its loads first (L2 hits), then the first frames' words
     // (HBM), then the image's LDS writes -- the frames' latency overlaps the
     // staging instead of following it
@@ -1080,7 +523,6 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     for (int t = 0; t < 16; t++)
         asm volatile("" : "+v"(w0[t]));
 
-#endif
     const float invL = 1.0f / 2048.0f;
 
     // one iteration per workgroup (grid = ceil(B / 16)): no value lives across
@@ -1186,7 +628,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         // weighted scores [p][KPAD] f2 (frame hw in component hw) in the wave's
         // tile space, lanes split the distinct lag tuples (4 consecutive per
         // lane and step, ascending: a strict '>' keeps the first maximum)
-        wave_lds_order();  // after the last pair's row reads of these tiles
+        wave_lds_sync();  // after the last pair's row reads of these tiles
         float *wsc = (float *)wtiles;  // [P][KPAD][2]
         const int gres = lane_res_sel(fresh_tid() & 31);
         const int gla = 2 * gres, glb = 2 * gres - 64;
@@ -1200,7 +642,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                     wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
         if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
             wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
-        wave_lds_order();  // the gathers read other lanes' score slots
+        wave_lds_sync();  // the gathers read other lanes' score slots
         LEAN_MARK();
         float gv[2] = {-INFINITY, -INFINITY};
         int gu[2] = {INT_MAX, INT_MAX};
@@ -1310,42 +752,12 @@ extern "C" int tdoa_diag_fetch_p1k(unsigned long long *host, int n)
 
 // --------------------------------------------------------------- host side
 namespace {
-template <int NW, bool DUAL>
+constexpr int P1K_NW = 8;  // waves per workgroup (two per SIMD)
+
 constexpr size_t p1k_lds(int U)
 {
-    return (size_t)NW * p1k_wave_lds<DUAL>() + 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4 +
+    return (size_t)P1K_NW * P1K_WAVE_LDS + P1K_IMG_FIXED +
            (size_t)(U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64) * 4;
-}
-
-int g_p1k_waves = -1;  // 0: use the generic kernels (A/B), else NW
-
-template <int NW, bool DUAL>
-int launch_p1k(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
-               float e2, hipStream_t st)
-{
-    const size_t lds = p1k_lds<NW, DUAL>(kp.U);
-    const void *kern = DUAL ? (const void *)k_phat1024<NW, DUAL> : (const void *)k_p1k_lean;
-    const int c_resident = tdoa_resident_blocks(kern, NW * 64, lds);
-    constexpr int NF = 2 * NW;
-    const int64_t groups = (B + NF - 1) / NF;
-    const int64_t iters = (groups + c_resident - 1) / c_resident;
-    // the one-wave kernel is persistent; the lean kernel does one group of
-    // 16 frames per workgroup
-    const int64_t grid = DUAL ? (groups + iters - 1) / iters : groups;
-    if (grid > 0x7FFFFFFF)
-        return tdoa_set_error(-1, "k_phat1024: batch too large for one launch");
-    if constexpr (DUAL)
-        hipLaunchKernelGGL((k_phat1024<NW, DUAL>), dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out,
-                           frames, B, e2);
-    else
-        hipLaunchKernelGGL(k_p1k_lean, dim3((unsigned)grid), dim3(NW * 64), lds, st, kp, out, frames, B, e2);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        char buf[256];
-        snprintf(buf, sizeof buf, "k_phat1024 launch: %s", hipGetErrorString(e));
-        return tdoa_set_error(-2, buf);
-    }
-    return 0;
 }
 }  // namespace
 
@@ -1394,19 +806,11 @@ void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int3
 // config-2 shape (M = 3, N = 1024, S <= 63) with a tuple table that fits the tail
 bool tdoa_phat1024_fits(const tdoa_kparams &kp)
 {
-    if (g_p1k_waves < 0) {
-        const char *s = getenv("TDOA_PHAT1024_WAVES");
-        g_p1k_waves = s ? atoi(s) : 8;
-        if (g_p1k_waves != 0 && g_p1k_waves != 4 && g_p1k_waves != 8)
-            g_p1k_waves = 8;
-    }
-    if (g_p1k_waves == 0 || kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1 || !kp.p1k_img)
+    if (kp.M != 3 || kp.N != 1024 || kp.S > 63 || kp.TW != 1 || !kp.p1k_img)
         return false;
-    // grid scores of a wave's four frames live in its tiles: [3][KPAD] float4 = 6 KiB
-    static_assert(3 * P1K_KPAD * 16 <= p1k_wave_lds<false>(), "grid scores exceed the wave's tiles");
-    if (g_p1k_waves == 8)
-        return p1k_lds<8, false>(kp.U) + 64 <= 160 * 1024;  // + the static progress words
-    return p1k_lds<4, true>(kp.U) <= 160 * 1024;
+    // grid scores of a wave's two frames live in its tiles: [3][KPAD] float2 = 3 KiB
+    static_assert(3 * P1K_KPAD * 8 <= P1K_WAVE_LDS, "grid scores exceed the wave's tiles");
+    return p1k_lds(kp.U) + 64 <= 160 * 1024;  // + the static progress words
 }
 
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
@@ -1417,7 +821,20 @@ int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int
     float e2 = phat_eps * 4294967296.0f;
     if (!(e2 >= 1e-30f))
         e2 = 1e-30f;
-    hipStream_t st = (hipStream_t)stream;
-    return g_p1k_waves == 4 ? launch_p1k<4, true>(kp, out, frames, B, e2, st)
-                            : launch_p1k<8, false>(kp, out, frames, B, e2, st);
+    if (B <= 0)
+        return 0;
+    // one workgroup of 16 frames (8 waves, one frame per half-wave) per group
+    constexpr int NF = 2 * P1K_NW;
+    const int64_t grid = (B + NF - 1) / NF;
+    if (grid > 0x7FFFFFFF)
+        return tdoa_set_error(-1, "k_p1k_lean: batch too large for one launch");
+    hipLaunchKernelGGL(k_p1k_lean, dim3((unsigned)grid), dim3(P1K_NW * 64), p1k_lds(kp.U), (hipStream_t)stream,
+                       kp, out, frames, B, e2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "k_p1k_lean launch: %s", hipGetErrorString(e));
+        return tdoa_set_error(-2, buf);
+    }
+    return 0;
 }

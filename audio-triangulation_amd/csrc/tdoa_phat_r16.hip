@@ -34,9 +34,7 @@
 
 // the long-frame kernels measured faster with the asm constant-twiddle
 // products (k_frame16<2048, 8>: 123.4 vs 127.4 ms per 1e6 frames)
-#ifndef R16_VEC_MUL_S
-#define TDOA_ASM_MUL_S 1
-#endif
+#define TDOA_ASM_MUL_S 1  // pinned asm twiddle products (tdoa_cplx.h)
 #include "tdoa_cplx.h"
 #include "tdoa_internal.h"
 #include "tdoa_keys.h"
@@ -931,18 +929,14 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
     hipStream_t st = (hipStream_t)stream;
     // the per-frame fused kernel (spectra on chip) for M = 3, 4 at frame_len 4096
     // and M = 4, 8 at 2048 (config 3: 6.41 vs 7.86 ms per 65536 frames, config
-    // 4: 161 vs 198 ms per 1e6); TDOA_PHAT_FUSED=0 keeps the two-pass kernels
-    static const int use_fused = [] {
-        const char *s = getenv("TDOA_PHAT_FUSED");
-        return s ? atoi(s) : 1;
-    }();
-    if (use_fused && kp.N == 4096 && kp.M == 4)
+    // 4: 161 vs 198 ms per 1e6); other mic counts take the two-pass kernels
+    if (kp.N == 4096 && kp.M == 4)
         return launch_frame16<4096, 4>(kp, out, frames, B, e2, st);
-    if (use_fused && kp.N == 4096 && kp.M == 3)
+    if (kp.N == 4096 && kp.M == 3)
         return launch_frame16<4096, 3>(kp, out, frames, B, e2, st);
-    if (use_fused && kp.N == 2048 && kp.M == 8)
+    if (kp.N == 2048 && kp.M == 8)
         return launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
-    if (use_fused && kp.N == 2048 && kp.M == 4)
+    if (kp.N == 2048 && kp.M == 4)
         return launch_frame16<2048, 4>(kp, out, frames, B, e2, st);
     return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)
                         : launch_r16<2048>(kp, out, frames, B, e2, scratch, scratch_bytes, st);

@@ -74,7 +74,8 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
 {
     const tdoa_stream_params &sp = st->sp;
     S_TRY(hipMemsetAsync(sp.count, 0, sizeof(int32_t), s));
-    int rc = tdoa_launch_stream_trigger(sp, st->S, s);
+    bool by_id = false;  // where the trigger put the frames: the layout DIRECT reads
+    int rc = tdoa_launch_stream_trigger(sp, st->S, s, &by_id);
     if (rc)
         return rc;
     tdoa_kout ko{};
@@ -82,7 +83,7 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
     ko.gate = sp.fresh_gate;
     ko.weighted = sp.fresh;
     tdoa_kparams kp = st->kp;
-    kp.frame_ids = tdoa_stream_trigger_by_id(sp, st->S) ? sp.ids : nullptr;
+    kp.frame_ids = by_id ? sp.ids : nullptr;
     rc = tdoa_launch_direct(kp, ko, sp.frames, st->S, false, s, nullptr, sp.count);
     if (rc)
         return rc;

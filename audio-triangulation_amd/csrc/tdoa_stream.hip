@@ -208,166 +208,13 @@ __device__ __forceinline__ int wave_scan_incl(int v)
     return v;
 }
 
-template <int G, int M>
-__global__ void __launch_bounds__(256) k_stream_trigger_w(tdoa_stream_params sp, int64_t S)
-{
-    constexpr int H = 64 * G, N = 2 * H, CB = G * M, CW = (CB + 3) / 4;
-    const int lane = threadIdx.x & 63;
-    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (s >= S)
-        return;  // whole wave: no workgroup barrier below
-    const int64_t pos = *sp.pos;       // samples consumed before this hop
-    const int64_t base = pos + 1 - N;  // stream index of local sample 0
-    const int64_t cl = sp.capture_len;
-    const uint8_t *cap = sp.capture + (size_t)s * cl * M;
-    int64_t j0 = base % cl;
-    if (j0 < 0)
-        j0 += cl;
-
-    // x[r][w]: the chunk's CB bytes (sample i, mic m at byte i M + m), packed
-    uint32_t x[3][CW];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        const int64_t l0 = base + r * H + G * lane;  // stream index of the chunk
-        int64_t j = j0 + r * H + G * lane;
-        if (j >= cl)
-            j -= cl;
-        // contiguous, and the aligned word reads (up to 7 bytes past the chunk)
-        // stay inside this stream's ring.  Word pointer and byte shift both come
-        // from the ABSOLUTE address: a stream's ring starts at s * cl * M, which
-        // need not be 4-byte aligned (M = 3 with an odd capture length); the
-        // aligned start may then lie up to 3 bytes before the ring (inside the
-        // previous stream's, the allocation's base being 4-byte aligned)
-        if (l0 >= 0 && (j + G) * M + 7 <= cl * M) {
-            const uintptr_t p = (uintptr_t)(cap + (size_t)j * M);
-            const uint32_t *wp = reinterpret_cast<const uint32_t *>(p & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)(p & 3u);
-            uint32_t w[CW + 1];
-#pragma unroll
-            for (int k = 0; k <= CW; k++)
-                w[k] = wp[k];
-#pragma unroll
-            for (int k = 0; k < CW; k++)
-                x[r][k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-        } else {  // stream start (zeros) or the ring's end
-#pragma unroll
-            for (int k = 0; k < CW; k++)
-                x[r][k] = 0;
-#pragma unroll
-            for (int i = 0; i < G; i++) {
-                int64_t ji = j + i;
-                if (ji >= cl)
-                    ji -= cl;
-#pragma unroll
-                for (int m = 0; m < M; m++) {
-                    const int b = i * M + m;
-                    const uint32_t v = l0 + i < 0 ? 0u : (uint32_t)cap[(size_t)ji * M + m];
-                    x[r][b >> 2] |= v << (8 * (b & 3));
-                }
-            }
-        }
-    }
-    auto smp = [&](int r, int i, int m) -> int {
-        const int b = i * M + m;
-        return (int)((x[r][b >> 2] >> (8 * (b & 3))) & 0xFFu);
-    };
-    // exclusive prefix at each chunk start: sum x per mic, sum x^2 over mics
-    int q1[3][M], q2[3];
-    {
-        int tot1[M], tot2 = 0;
-#pragma unroll
-        for (int m = 0; m < M; m++)
-            tot1[m] = 0;
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            int c2 = 0;
-#pragma unroll
-            for (int m = 0; m < M; m++) {
-                int c1 = 0;
-#pragma unroll
-                for (int i = 0; i < G; i++) {
-                    const int v = smp(r, i, m);
-                    c1 += v;
-                    c2 += v * v;
-                }
-                const int inc = wave_scan_incl(c1);
-                q1[r][m] = tot1[m] + inc - c1;
-                tot1[m] += __builtin_amdgcn_readlane(inc, 63);
-            }
-            const int inc2 = wave_scan_incl(c2);
-            q2[r] = tot2 + inc2 - c2;
-            tot2 += __builtin_amdgcn_readlane(inc2, 63);
-        }
-    }
-    // candidates a = G lane + i in ascending order: powers of the older and
-    // newer halves, summed over mics; the first firing one
-    constexpr int hb = __builtin_ctz(N) - 1;
-    const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
-    const int64_t amin = sp.ring_start[s] + N - pos - 1;  // full ring: >= N samples since the last trigger
-    int fi = -1;
-#pragma unroll
-    for (int i = 0; i < G; i++) {
-        const int a = G * lane + i;
-        long long pout = (long long)(q2[1] - q2[0]) << hb, pin = (long long)(q2[2] - q2[1]) << hb;
-#pragma unroll
-        for (int m = 0; m < M; m++) {
-            const long long so1 = q1[1][m] - q1[0][m], si1 = q1[2][m] - q1[1][m];
-            pout -= so1 * so1;
-            pin -= si1 * si1;
-        }
-        if (fi < 0 && a >= amin && pout > thr + pin)
-            fi = i;
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-#pragma unroll
-            for (int m = 0; m < M; m++) {
-                const int v = smp(r, i, m);
-                q1[r][m] += v;
-                q2[r] += v * v;
-            }
-        }
-    }
-    const uint64_t fire = __ballot(fi >= 0);
-    if (fire == 0)
-        return;
-    const int fl = __builtin_ctzll(fire);  // lowest lane = lowest candidates
-    const int a = G * fl + __builtin_amdgcn_readlane(fi, fl);
-    int slot = 0;
-    if (lane == 0) {
-        slot = atomicAdd(sp.count, 1);
-        const int64_t end = pos + 1 + a;
-        sp.ids[slot] = (int32_t)s;
-        sp.end[slot] = end;
-        sp.ring_start[s] = end;
-    }
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    // the frame: local samples a .. a + N - 1 of every mic (rolling_buffer.c:48-62 order)
-    int16_t *dst = sp.frames + (size_t)slot * M * N;
-    int64_t ja = j0 + a + lane;
-    if (ja >= cl)
-        ja -= cl;
-#pragma unroll 4
-    for (int t = 0; t < N / 64; t++) {
-        const int n = lane + 64 * t;
-        int64_t jn = ja + 64 * t;
-        while (jn >= cl)
-            jn -= cl;
-        const bool neg = base + a + n < 0;
-#pragma unroll
-        for (int m = 0; m < M; m++)
-            dst[(size_t)m * N + n] = neg ? (int16_t)0 : (int16_t)cap[(size_t)jn * M + m];
-    }
-}
-
-// Persistent form of k_stream_trigger_w (same scan, same results): each wave
-// walks streams gw, gw + GW, ... with the NEXT stream's capture words and ring
-// start already requested while it scans the current one (the one-stream-per-
-// wave kernel waited on its loads at the start of every wave: 68 % of wave
-// cycles in SQ_WAIT_ANY).  A firing stream's frame is written from the words
-// the wave already holds, staged through LDS (no second read of the ring).
-#ifndef TRIG_NWB
-#define TRIG_NWB 4  // waves per workgroup: occupancy in steps of one wave per SIMD
-#endif
+// Persistent: each wave walks streams gw, gw + GW, ... with the NEXT stream's
+// capture words and ring start already requested while it scans the current one
+// (a one-stream-per-wave form waited on its loads at the start of every wave:
+// 68 % of wave cycles in SQ_WAIT_ANY).  A firing stream's frame is written from
+// the words the wave already holds, staged through LDS (no second read of the
+// ring).
+constexpr int TRIG_NWB = 4;  // waves per workgroup: occupancy in steps of one wave per SIMD
 template <int G, int M>
 __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
 {
@@ -440,7 +287,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
                 // the kernel's register count)
                 const int64_t l0 = base + r * H + G * lane;
                 uint8_t *sb8 = reinterpret_cast<uint8_t *>(stage) + r * H * M + lane * CB;
-                __builtin_amdgcn_wave_barrier();  // the previous stream's stage reads come first
+                wave_lds_sync();  // the previous stream's stage reads come first
 #pragma unroll 1
                 for (int b = 0; b < CB; b++) {
                     const int i = b / M, m = b - i * M;
@@ -449,7 +296,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
                         ji -= cl;
                     sb8[b] = l0 + i < 0 ? (uint8_t)0 : cap[(size_t)ji * M + m];
                 }
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_sync();
 #pragma unroll
                 for (int k = 0; k < CW; k++)
                     x[r][k] = stage[r * (H * M / 4) + lane * CW + k];
@@ -566,13 +413,13 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
                 sp.ring_start[s] = end;
             // the frame (local samples a .. a + N - 1 of every mic, rolling_buffer.c:48-62
             // order) from the words in registers: rows 0..2 staged as [l][m] bytes
-            __builtin_amdgcn_wave_barrier();  // the previous stream's stage reads come first
+            wave_lds_sync();  // the previous stream's stage reads come first
 #pragma unroll
             for (int r = 0; r < 3; r++)
 #pragma unroll
                 for (int k = 0; k < CW; k++)
                     stage[r * (H * M / 4) + lane * CW + k] = x[r][k];
-            __builtin_amdgcn_wave_barrier();  // a wave's LDS operations complete in order
+            wave_lds_sync();  // a wave's LDS operations complete in order
             const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
             // at the stream's own index: the compact list (ids, end) is
             // written once per workgroup at the end (thousands of same-address
@@ -607,8 +454,6 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
         sp.end[o + lane] = my_end;
     }
 }
-
-int g_trigger_p = -1;  // TDOA_TRIGGER_P=0: one stream per wave (k_stream_trigger_w)
 
 // correlations.c:40-43 in the reference's float/double steps
 __device__ __forceinline__ float decay_us(uint64_t now, uint64_t last)
@@ -812,20 +657,13 @@ size_t tdoa_stream_trigger_lds(int M, int N, int H)
     return ((M * L * 2 + 15) & ~(size_t)15) + (((L + 1) * 4 + 15) & ~(size_t)15) + (L + 1) * 8;
 }
 
-// the persistent register scan applies (and writes frames by stream id)
-static bool trigger_p_applies(const tdoa_stream_params &sp, int64_t S, int *res_out)
+// the persistent register scan applies (N = 2H, config 5: N 1024, hop 512;
+// aligned capture); it writes each frame at its stream's index
+static bool trigger_p_applies(const tdoa_stream_params &sp)
 {
-    if (g_trigger_p < 0) {
-        const char *e = getenv("TDOA_TRIGGER_P");
-        g_trigger_p = e ? atoi(e) : 1;
-    }
-    if (!g_trigger_p || !(sp.N == 2 * sp.H && ((uintptr_t)sp.capture & 3) == 0 &&
-                          sp.capture_len >= (int64_t)sp.N + 2 * sp.H))
-        return false;
-    if (!(sp.H == 256 || sp.H == 512 || sp.H == 1024) || sp.M < 2 || sp.M > 4)
-        return false;
-    (void)res_out;
-    return true;
+    return sp.N == 2 * sp.H && ((uintptr_t)sp.capture & 3) == 0 &&
+           sp.capture_len >= (int64_t)sp.N + 2 * sp.H && (sp.H == 256 || sp.H == 512 || sp.H == 1024) &&
+           sp.M >= 2 && sp.M <= 4;
 }
 
 template <int G, int M>
@@ -845,59 +683,37 @@ static void launch_trigger_p(const tdoa_stream_params &sp, int64_t S, hipStream_
 }
 
 template <int G>
-static bool launch_trigger_w(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
+static void launch_trigger_m(const tdoa_stream_params &sp, int64_t S, hipStream_t st)
 {
-    if (trigger_p_applies(sp, S, nullptr)) {
-        if (sp.M == 2)
-            launch_trigger_p<G, 2>(sp, S, st);
-        else if (sp.M == 3)
-            launch_trigger_p<G, 3>(sp, S, st);
-        else if (sp.M == 4)
-            launch_trigger_p<G, 4>(sp, S, st);
-        else
-            return false;
-        return true;
-    }
-    const dim3 grid((unsigned)((S + 3) / 4));
     if (sp.M == 2)
-        hipLaunchKernelGGL((k_stream_trigger_w<G, 2>), grid, dim3(256), 0, st, sp, S);
+        launch_trigger_p<G, 2>(sp, S, st);
     else if (sp.M == 3)
-        hipLaunchKernelGGL((k_stream_trigger_w<G, 3>), grid, dim3(256), 0, st, sp, S);
-    else if (sp.M == 4)
-        hipLaunchKernelGGL((k_stream_trigger_w<G, 4>), grid, dim3(256), 0, st, sp, S);
+        launch_trigger_p<G, 3>(sp, S, st);
     else
-        return false;
-    return true;
+        launch_trigger_p<G, 4>(sp, S, st);
 }
 
-bool tdoa_stream_trigger_by_id(const tdoa_stream_params &sp, int64_t S)
+int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream, bool *by_id)
 {
-    return trigger_p_applies(sp, S, nullptr);
-}
-
-int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *stream)
-{
-    // register scan when N = 2H (config 5: N 1024, hop 512), aligned capture
-    if (sp.N == 2 * sp.H && ((uintptr_t)sp.capture & 3) == 0 && sp.capture_len >= (int64_t)sp.N + 2 * sp.H) {
-        hipStream_t st = (hipStream_t)stream;
-        bool ok = false;
+    hipStream_t st = (hipStream_t)stream;
+    if (trigger_p_applies(sp)) {
         if (sp.H == 256)
-            ok = launch_trigger_w<4>(sp, S, st);
+            launch_trigger_m<4>(sp, S, st);
         else if (sp.H == 512)
-            ok = launch_trigger_w<8>(sp, S, st);
-        else if (sp.H == 1024)
-            ok = launch_trigger_w<16>(sp, S, st);
-        if (ok) {
-            hipError_t e = hipGetLastError();
-            return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger_w launch");
-        }
+            launch_trigger_m<8>(sp, S, st);
+        else
+            launch_trigger_m<16>(sp, S, st);
+        *by_id = true;  // frames at their streams' indices, read through the id list
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger_p launch");
     }
+    *by_id = false;  // frames in compact slots
     if (sp.H > TPB * MAX_CAND)
         return tdoa_set_error(-1, "stream: hop too large");
     const size_t lds = tdoa_stream_trigger_lds(sp.M, sp.N, sp.H);
     if (lds > 150 * 1024)
         return tdoa_set_error(-1, "stream: (frame_len + hop) x mics exceeds the LDS budget");
-    hipLaunchKernelGGL(k_stream_trigger, dim3((unsigned)S), dim3(TPB), lds, (hipStream_t)stream, sp);
+    hipLaunchKernelGGL(k_stream_trigger, dim3((unsigned)S), dim3(TPB), lds, st, sp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger launch");
 }

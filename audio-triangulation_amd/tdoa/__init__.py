@@ -17,7 +17,7 @@ def __getattr__(name):
     if name == "Localizer":
         from .localizer import Localizer
         return Localizer
-    if name in ("synth", "reference", "localizer"):
+    if name in ("synth", "localizer", "stream", "shard"):
         import importlib
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

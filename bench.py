@@ -69,12 +69,9 @@ CONFIGS = {
 
 def dominant_kernel(config: int, engine: str) -> str:
     """Name of the kernel(s) a launch runs (the ones `traffic` was measured on)."""
-    if config == 2 and engine == "gcc_phat":
-        w = os.environ.get("TDOA_PHAT1024_WAVES", "8")
-        return {"8": "k_p1k_lean", "4": "k_phat1024"}.get(w, "k_gcc_phat_1024")
     if config == 2:
-        return "k_direct_mfma" if os.environ.get("TDOA_DIRECT_MFMA", "1") != "0" else "k_direct"
-    if config in (3, 4) and engine == "gcc_phat" and os.environ.get("TDOA_PHAT_FUSED", "1") != "0":
+        return "k_p1k_lean" if engine == "gcc_phat" else "k_direct_mfma"
+    if config in (3, 4) and engine == "gcc_phat":
         return "k_frame16 + k_grid_bb"
     return ""
 
@@ -105,6 +102,9 @@ def parse():
                          "the rotating batches' translations settle, so a short K-step window "
                          "measures the steady state; 0 disables")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: rehearse the N-process launch, rank logic and JSON line over gloo "
+                         "with a stand-in CPU step (tests/test_distributed.py); not a measurement")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--also", action="store_true", help="also time the other engine")
     ap.add_argument("--no-grid", action="store_true", help="diagnostic: skip the grid solve")
@@ -170,9 +170,20 @@ def parity_report(engine, loc, frames, tau, out):
         rep["lags_equal_direct"] = float(same.mean())
         rep["frames_all_lags_equal_direct"] = float(same.all(-1).mean())
         if "cell" in got:
-            rep["cells_equal_direct"] = float((got["cell"] == dref["cell"]).mean())
+            same_c = got["cell"] == dref["cell"]
+            rep["cells_equal_direct"] = float(same_c.mean())
+            # how far the disagreeing frames' (x, y) lie from DIRECT's, in metres
+            d = np.hypot(*(got["xy"] - dref["xy"]).T)
+            dd = d[~same_c]
+            rep["xy_distance_to_direct_m"] = {
+                "p50": float(np.percentile(dd, 50)) if dd.size else 0.0,
+                "p99": float(np.percentile(dd, 99)) if dd.size else 0.0,
+                "max": float(dd.max()) if dd.size else 0.0,
+                "over": "frames whose cell differs from DIRECT's", "frames": int(dd.size)}
         rep["contract"] = ("lags equal DIRECT wherever the fp64 GCC-PHAT top-2 margin exceeds "
-                           "2e-4 (tests/test_gpu_gcc_phat.py); DIRECT is bit-exact with the oracle")
+                           "2e-4; cell agreement with DIRECT and the disagreements' distances "
+                           "bounded per shape (tests/test_gpu_gcc_phat.py); DIRECT is bit-exact "
+                           "with the oracle")
     else:
         rep["contract"] = "DIRECT is bit-exact with the oracle (tests/test_gpu_parity.py)"
     rep["pairs"] = int(P)
@@ -196,7 +207,9 @@ def time_engine(engine, args, dev, ri, cache):
                               shard.frame_seed(0x5EED0000 + args.config, ri.rank, r), dev)
         batches.append(fr)
         taus.append(tau)
-    out = loc.alloc_outputs(B, grid=not args.no_grid)
+    # config 4 is "28 pairs + least-squares": the LS refinement runs in the timed region
+    ls = args.config == 4 and not args.no_grid
+    out = loc.alloc_outputs(B, grid=not args.no_grid, ls=ls)
     stream = torch.cuda.current_stream(dev)
     # preflight (untimed, before the W warmups): every rotating batch once, then
     # until preflight_s has passed (bounded); reported in the line
@@ -215,7 +228,8 @@ def time_engine(engine, args, dev, ri, cache):
                     on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # GPU time per launch, launch stream
     total = shard.sum_over_ranks([B * args.steps], device=dev)[0]
-    bytes_per_loc = M * N * 2 + 4 * P + 8
+    # algorithmic bytes: frames in, lags + (x, y) out (+ xy_ls and its rms with LS)
+    bytes_per_loc = M * N * 2 + 4 * P + 8 + (12 if ls else 0)
     res = {
         "engine": engine,
         "value": total / t["wall_max_s"],
@@ -227,6 +241,7 @@ def time_engine(engine, args, dev, ri, cache):
         "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
         "rotate_batches": R,
         "preflight_steps": pre_n,
+        "ls": ls,
     }
     lags = out["lags"].cpu()
     assert int(lags.abs().max()) <= loc.dims.S
@@ -404,7 +419,7 @@ def main_config1(args, dev, ri):
             "roofline": None,
             "note": "latency-bound plumbing: seven synchronous GPU-backed calls per frame "
                     "(the batched API is configs 2-5)",
-            "cpu_baseline": cpu_baseline_config1(args, res) if world == 1 and not args.no_cpu else None,
+            "cpu_baseline": cpu_baseline_config1(args, res) if not args.no_cpu else None,
         }
         print(json.dumps(line), flush=True)
     shard.finalize()
@@ -522,9 +537,83 @@ def stream_traffic(args):
                       "read = 2 x FETCH_SIZE; the trigger re-reads the two previous hops")
 
 
+def launch_workers(args):
+    """--gpus N > 1 outside a torch.distributed launch: start the N rank
+    processes (one per GPU) through torch.distributed.run as a CHILD process,
+    before this process has touched a GPU, and return its exit code.  None:
+    this process is a rank of a launch (or N = 1) and runs the bench itself."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args, where):
+    """The ranks that joined must be the ranks asked for (--gpus)."""
+    seen = shard.ranks_seen()
+    if seen != args.gpus:
+        print(f"bench.py: {where}: {seen} ranks joined, --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(3)
+    return seen
+
+
+def rehearse(args):
+    """--cpu-rehearsal: the N-rank path without a GPU -- the self-launch, the
+    gloo process group, the rank logic of tdoa/shard.py (per-rank batches,
+    the timed bracket, max over ranks, sums), the JSON line and the rank-0
+    cpu_baseline -- with a stand-in CPU step (a byte sum over the rank's
+    frames).  Its value measures nothing and says so."""
+    ri = shard.init_distributed("gloo")
+    world = check_world(args, "rehearsal")
+    cfg = CONFIGS[2]
+    B = shard.rank_frames(64, ri.rank, ri.world, cfg["scaling"])
+    rng = np.random.default_rng(shard.frame_seed(0x5EED0002, ri.rank))
+    fr = rng.integers(0, 256, (B, cfg["M"], cfg["N"]), dtype=np.int16)
+    t = shard.timed(lambda k: int(fr.sum()), args.steps, args.warmup)
+    total = shard.sum_over_ranks([B * args.steps])[0]
+    if ri.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        import tdoa
+        lut = O.build_lut(O.microphones_ref(), fs=50000, max_shift=46)
+        line = {"metric": "REHEARSAL (no GPU, stand-in CPU step): rank logic of "
+                          "'GCC-PHAT localizations/sec, 3-mic x 1024-sample frames'",
+                "value": total / t["wall_max_s"], "unit": "frames/s (stand-in step)",
+                "n_gpus": 0, "ranks_seen": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": t["wall_max_s"] * 1e3 / args.steps, "higher_is_better": True,
+                "scaling": cfg["scaling"], "vs_baseline": None, "dtype": "none",
+                "data": "rehearsal: random bytes, byte-sum step", "rehearsal": True,
+                "config": {"workload": "rehearsal of the config-2 rank logic", "batch_per_rank": B,
+                           "parallelism": f"dp{world} (gloo, CPU)"},
+                "roofline": None,
+                "cpu_baseline": None if args.no_cpu else cpu_baseline(
+                    args, lut.reshape(3, -1), tdoa.dpss_q15(1024))}
+        print(json.dumps(line), flush=True)
+    shard.finalize()
+
+
 def main():
     args = parse()
+    rc = launch_workers(args)  # before anything touches a GPU
+    if rc is not None:
+        sys.exit(rc)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        print(f"bench.py: WORLD_SIZE {env_world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(3)
+    if args.cpu_rehearsal:
+        return rehearse(args)
     ri = shard.init_distributed("nccl")
+    check_world(args, "process group")
     dev = torch.device("cuda", ri.local_rank)
     torch.cuda.set_device(dev)
     cache = {}
@@ -567,7 +656,8 @@ def main():
                     "synthetic (ADC-like u8 frames, injected integer delays, generated on the GPU, "
                     "resident in HBM; one batch larger than the 256 MiB Infinity Cache)",
             "config": {"workload": f"{cfg['desc']}, {B} frames per GPU per step, "
-                                   "xcorr + lag prior + (x,y) grid",
+                                   "xcorr + lag prior + (x,y) grid"
+                                   + (" + least-squares (x,y)" if main_res["ls"] else ""),
                        "engine": args.engine, "batch_per_gpu": B,
                        "global_batch": args.batch if cfg["scaling"] == "strong" else B * world,
                        "mics": cfg["M"], "frame_len": cfg["N"],
@@ -591,7 +681,7 @@ def main():
         if other is not None:
             other.pop("parity", None)
             line["other_engine"] = other
-        if world == 1 and not args.no_cpu:
+        if not args.no_cpu:  # rank 0, after the timed region, at every world size
             line["cpu_baseline"] = cpu_baseline(args, cache["lut"], cache["window"])
         print(json.dumps(line), flush=True)
     shard.finalize()
@@ -632,7 +722,7 @@ def main_stream(args, dev, ri, cache):
                          "bytes_per_step": res["capture_bytes_per_step"] // ri.world},
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu:
+        if not args.no_cpu:  # rank 0, after the timed region, at every world size
             line["cpu_baseline"] = cpu_baseline_stream(args, cache["lut"], cache["window"],
                                                        cache["S"])
         print(json.dumps(line), flush=True)

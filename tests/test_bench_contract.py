@@ -46,11 +46,12 @@ def test_traffic_only_for_dispatched_kernels():
     t2, src = bench.traffic_entry(_args())
     assert t2 == tj["c2_gcc_phat"]["hbm_bytes_per_launch"] and "k_p1k_lean" in src
     # a kernel the committed passes were not taken on: no traffic figure
-    os.environ["TDOA_PHAT1024_WAVES"] = "4"
+    real = bench.dominant_kernel
+    bench.dominant_kernel = lambda config, engine: "k_not_profiled"
     try:
         assert bench.traffic_entry(_args()) == (None, None)
     finally:
-        del os.environ["TDOA_PHAT1024_WAVES"]
+        bench.dominant_kernel = real
     for cfg in (3, 4):
         t, src = bench.traffic_entry(_args("--config", str(cfg)))
         ks = tj[f"c{cfg}_gcc_phat"]["kernels"]

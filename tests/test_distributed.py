@@ -107,3 +107,38 @@ def test_single_process_defaults():
     assert (ri.rank, ri.world) == (0, 1) and shard.ranks_seen() == 1
     assert shard.max_over_ranks(3.5) == 3.5 and shard.sum_over_ranks([2, 3]) == [2.0, 3.0]
     assert shard.rank_frames(10, 0, 1, "strong") == 10
+
+
+def _bench(*argv, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launches_two_ranks():
+    """`python bench.py --gpus 2` (no torchrun around it) starts its two rank
+    processes itself, before touching a GPU; here over gloo with the stand-in
+    CPU step of --cpu-rehearsal.  One JSON line: both ranks joined, and the
+    rank-0 cpu_baseline is attached at N > 1 too."""
+    import json
+    r = _bench("--gpus", "2", "--cpu-rehearsal", "--steps", "3", "--warmup", "1",
+               "--cpu-seconds", "0.5")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["ranks_seen"] == 2 and d["rehearsal"] is True and d["steps"] == 3
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+
+
+def test_bench_refuses_a_world_that_is_not_gpus():
+    """A launch whose WORLD_SIZE differs from --gpus exits non-zero instead of
+    timing the wrong number of GPUs."""
+    r = _bench("--gpus", "2", "--cpu-rehearsal", env_extra={"WORLD_SIZE": "1"}, timeout=120)
+    assert r.returncode == 3 and "--gpus 2" in r.stderr

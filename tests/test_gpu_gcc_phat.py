@@ -158,6 +158,9 @@ PHAT_CONFIGS = [
     (4, 2048, 67600, synth.square_mics(0.15), 40),         # S = 63: lags -63..63, the widest K
     (5, 1024, 50000, synth.circle_mics(5, 0.15), 64),
     (4, 256, 50000, synth.square_mics(0.15), 64),
+    # the reference triangle doubled, S = 63: 6510 distinct lag tuples, more
+    # than k_p1k_lean's LDS tail holds -> the generic fused k_gcc_phat_1024
+    (3, 1024, 67600, np.array([[-0.132, -0.076], [0.132, -0.076], [0.0, 0.152]], np.float32), 64),
 ]
 
 
@@ -255,3 +258,74 @@ def test_grid_bb_exact_on_own_scores(shape, kind):
     cell, mx = _grid_f32(got["weighted_f"], lut)
     assert (got["cell"] == cell).all()
     assert (got["max_Lf"] == mx).all()
+
+
+# ---- GCC-PHAT cell / (x, y) contract against DIRECT (the reference semantics:
+# the first row-major maximum of vga_heatmap.h:99-108 on the int64 weighted
+# scores of correlations.c:20-33).  The two engines score lags differently
+# (PHAT-whitened fp32 vs raw integer products), so their grid maxima can fall
+# on different cells where DIRECT's own L is nearly flat.  Contract per shape,
+# on ADC-like integer-delay frames (synth.adc_frames):
+#   agreement rate >= CELL_AGREE[shape]  (the measured rate minus a slack)
+#   every disagreeing frame: GCC's cell is a near-maximum of DIRECT's own L
+#     ((max L - L[gcc cell]) / |max L| <= CELL_L_GAP) or lies within
+#     CELL_RADIUS grid cells (Chebyshev) of DIRECT's cell
+CELL_SHAPES = {
+    "cfg2": dict(M=3, N=1024, mics=None, B=4096),
+    "cfg3": dict(M=4, N=4096, mics="square", B=2048),
+    "cfg4": dict(M=8, N=2048, mics="circle", B=2048),
+}
+CELL_AGREE = {"cfg2": 0.995, "cfg3": 0.94, "cfg4": 0.92}
+CELL_L_GAP = 0.05
+CELL_RADIUS = 3
+
+
+def _direct_L_at(weighted, lut, cells):
+    """DIRECT's int64 L (sum over pairs of weighted[p][lut[p][cell]]) at given cells."""
+    P = weighted.shape[1]
+    lut2 = np.asarray(lut).reshape(P, -1).astype(np.int64)
+    idx = lut2[:, cells].T  # [B][P]
+    return np.take_along_axis(weighted, idx[:, :, None], axis=2)[:, :, 0].sum(-1)
+
+
+@pytest.mark.parametrize("shape", sorted(CELL_SHAPES))
+def test_cell_contract_vs_direct(shape):
+    c = CELL_SHAPES[shape]
+    xy = {None: None, "square": synth.square_mics(0.15), "circle": synth.circle_mics(8, 0.15)}[c["mics"]]
+    kw = dict(num_mics=c["M"], frame_len=c["N"], mic_xy=xy)
+    ph = Localizer(engine="gcc_phat", **kw)
+    direct = Localizer(engine="direct", **kw)
+    lut = ph.lut()
+    fr, _, _ = synth.adc_frames(c["B"], c["M"], c["N"], lut.reshape(ph.dims.P, 101, 101), ph.dims.S,
+                                synth.SEEDS[{"cfg2": 2, "cfg3": 3, "cfg4": 4}[shape]], device="cuda")
+    got = _np(ph.localize(fr))
+    d = _np(direct.localize(fr, scores=True))
+    same = got["cell"] == d["cell"]
+    rate = same.mean()
+    L_gcc = _direct_L_at(d["weighted"], lut, got["cell"])
+    gap = (d["max_L"] - L_gcc) / np.maximum(np.abs(d["max_L"]), 1)
+    W = 101
+    cheb = np.maximum(np.abs(got["cell"] % W - d["cell"] % W), np.abs(got["cell"] // W - d["cell"] // W))
+    bad = ~same & ~(gap <= CELL_L_GAP) & ~(cheb <= CELL_RADIUS)
+    print(f"{shape}: cells equal {rate:.4f}; disagreements {int((~same).sum())}: "
+          f"L gap p50 {np.median(gap[~same]) if (~same).any() else 0:.4f} max {gap.max():.4f}, "
+          f"cells apart p50 {np.median(cheb[~same]) if (~same).any() else 0} max {cheb.max()}")
+    assert (gap >= 0).all()  # DIRECT's cell is DIRECT's maximum
+    assert rate >= CELL_AGREE[shape], rate
+    assert not bad.any(), np.argwhere(bad)[:5].ravel().tolist()
+    ph.close()
+    direct.close()
+
+
+def test_long_frames_big_grid_exhaustive():
+    """A 261 x 261 grid at 4 mics x 2048: more 8 x 8 blocks than k_grid_bb's
+    table holds -> the exhaustive float grid (k_grid) after k_frame16."""
+    loc = Localizer(engine="gcc_phat", num_mics=4, frame_len=2048, mic_xy=synth.square_mics(0.15),
+                    grid_half_w=130, grid_half_h=130)
+    lut = loc.lut()
+    fr, _, _ = synth.adc_frames(64, 4, 2048, lut.reshape(6, 261, 261), loc.dims.S, 0x261, device="cuda")
+    got = _np(loc.localize(fr, scores=True))
+    cell, mx = _grid_f32(got["weighted_f"], lut)
+    assert (got["cell"] == cell).all()
+    assert (got["max_Lf"] == mx).all()
+    loc.close()

@@ -102,6 +102,9 @@ CONFIGS = [
     (3, 1024, 67600, 63, np.array([[-0.132, -0.076], [0.132, -0.076], [0.0, 0.152]], np.float32), 50),
     # a 261 x 261 grid: more cells than the keyed grid's 16 index bits
     (3, 1024, 50000, 0, None, 130),
+    # 2 mics x 4096: frames exceed k_direct_mfma's staging registers -> the VALU
+    # k_direct and the separate int64 branch-and-bound grid (k_grid_bb<int64_t>)
+    (2, 4096, 50000, 0, np.array([[-0.066, 0.0], [0.066, 0.0]], np.float32), 50),
 ]
 
 
