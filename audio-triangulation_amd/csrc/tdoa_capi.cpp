@@ -216,6 +216,8 @@ struct tdoa_ctx {
     size_t rscratch_bytes = 0;
     void *d_cscratch = nullptr;
     size_t cscratch_bytes = 0;
+    void *d_tscratch = nullptr;  // [B][P][3] float peak scores (least squares)
+    size_t tscratch_bytes = 0;
     std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx
     void *d_bb = nullptr;
     int bb_NT = 0;
@@ -376,11 +378,14 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_wscratch);
     (void)hipFree(c->d_rscratch);
     (void)hipFree(c->d_cscratch);
+    (void)hipFree(c->d_tscratch);
     (void)hipFree(c->d_mic);
     (void)hipFree(c->d_lut);
     c->d_lut = nullptr;
     c->d_rscratch = c->d_cscratch = nullptr;
     c->rscratch_bytes = c->cscratch_bytes = 0;
+    c->d_tscratch = nullptr;
+    c->tscratch_bytes = 0;
     c->d_mic = nullptr;
     (void)hipFree(c->d_spec);
     c->d_spec = nullptr;
@@ -704,7 +709,7 @@ extern "C" int tdoa_get_dims(const tdoa_ctx *c, int32_t *M, int32_t *N, int32_t 
 
 static tdoa_kout to_kout(const tdoa_outputs *o)
 {
-    tdoa_kout k;
+    tdoa_kout k{};
     k.lags = o->lags;
     k.gate = o->gate;
     k.cell = o->cell;
@@ -774,7 +779,7 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     const size_t sz = phat ? sizeof(float) : sizeof(int64_t);
     const size_t pk = (size_t)B * ctx->P * ctx->K * sz;
     const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
-    const bool fused_grid = phat ? tdoa_gcc_phat_fused_grid(ctx->kp) : tdoa_direct_fused_grid(ctx->kp);
+    const bool fused_grid = phat ? tdoa_gcc_phat_grid_in_kernel(ctx->kp) : tdoa_direct_fused_grid(ctx->kp);
     if (grid && !weighted && !fused_grid) {
         // the grid kernel reads the weighted scores back: keep them in scratch
         int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, pk, stream, "weighted-score");
@@ -787,7 +792,17 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
             k.weighted = (int64_t *)ctx->d_wscratch;
     }
     const void *raw = phat ? (const void *)out->scores_f : (const void *)out->scores;
-    if (ls && !raw) {  // the refinement reads the raw scores around each peak
+    // the refinement's peak scores: from the kernel (it keeps the scores on
+    // chip) or from the raw scores around each peak
+    const bool peak_k = ls && phat && tdoa_gcc_phat_peak3(ctx->kp);
+    if (peak_k) {
+        int rc = grow(&ctx->d_tscratch, &ctx->tscratch_bytes, (size_t)B * ctx->P * 3 * sizeof(float), stream,
+                      "peak-score");
+        if (rc)
+            return rc;
+        k.peak3 = (float *)ctx->d_tscratch;
+    }
+    if (ls && !raw && !peak_k) {  // the refinement reads the raw scores around each peak
         int rc = grow(&ctx->d_rscratch, &ctx->rscratch_bytes, pk, stream, "raw-score");
         if (rc)
             return rc;
@@ -812,7 +827,7 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
         rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
     if (rc != 0 || !ls)
         return rc;
-    return tdoa_launch_ls(ctx->kp, raw, phat, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);
+    return tdoa_launch_ls(ctx->kp, raw, phat, k.peak3, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);
 }
 
 extern "C" int tdoa_heatmap(tdoa_ctx *ctx, const void *weighted, const void *max_L, int is_float,

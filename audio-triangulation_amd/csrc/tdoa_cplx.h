@@ -111,21 +111,15 @@ __device__ __forceinline__ f2 c_i(f2 x)
     return r;
 }
 
-// x / max(|x|, sqrt(e2)):  (x.x^2, x.y^2) -> |x|^2 in both dwords -> rsq -> scale
+// x / sqrt(|x|^2 + e2): |x|^2 + e2 as two fma (no clamp instruction; a zero
+// bin stays 0, and for every other bin of an integer frame e2 is far below the
+// fp32 resolution of |x|^2), rsq, scale.  The rsq lands in the low dword of a
+// pair whose high dword op_sel_hi ignores (no copy to build {r, r}).  The
+// multiply opens with s_nop 0: a transcendental result read by the next VALU
+// needs one wait state, and the compiler does not pad ahead of asm
 __device__ __forceinline__ f2 c_unit(f2 x, float e2)
 {
-    f2 t, s;
-    asm("v_pk_mul_f32 %1, %2, %2\n\t"
-        "v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]"
-        : "=v"(s), "=&v"(t)
-        : "v"(x));
-    // v_max without the canonicalising v_max x, x fmaxf adds (|x|^2 is never
-    // a NaN the clamp must quiet); the rsq lands in the low dword of a pair
-    // whose high dword op_sel_hi ignores (no copy to build {r, r}).  The
-    // multiply opens with s_nop 0: a transcendental result read by the next
-    // VALU needs one wait state, and the compiler does not pad ahead of asm
-    float m;
-    asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(s.x), "v"(e2));
+    const float m = __builtin_fmaf(x.x, x.x, __builtin_fmaf(x.y, x.y, e2));
     f2 rr;
     rr.x = __builtin_amdgcn_rsqf(m);
     f2 y;

@@ -669,6 +669,20 @@ bool tdoa_phat_r16_fits(int M, int N, int S);
 int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                          float phat_eps, void *scratch, size_t scratch_bytes, void *stream);
 
+bool tdoa_phat_r16_peak3(const tdoa_kparams &kp);
+
+bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
+
+// the launch solves the grid itself (no weighted-score scratch, no grid launch)
+bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp)
+{
+    return !tdoa_gcc_phat_needs_split(kp.M, kp.N) && tdoa_gcc_phat_fused_grid(kp);
+}
+
+// the launch writes the least-squares peak scores (kout.peak3) itself
+bool tdoa_gcc_phat_peak3(const tdoa_kparams &kp) { return tdoa_phat_r16_peak3(kp); }
+
+// the N = 1024, M = 3 kernels (k_p1k_lean, k_gcc_phat_1024) solve the grid
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp)
 {
     if (tdoa_phat1024_fits(kp))

@@ -23,6 +23,26 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The least-squares refinement's sub-sample lag (tdoa_ls.hip, oracle
+// orc_ls_refine): the argmax plus the parabolic vertex of the raw scores
+// y0, y1, y2 at lags best - 1, best, best + 1, clamped to +-0.5; none at the
+// lag range's ends (inside = false) or without a maximum (den >= 0).  One
+// definition for k_ls and the kernels that keep the scores on chip, rounded
+// as the C oracle (no contraction whatever the TU's flags).
+__device__ __forceinline__ double ls_tau3(double y0, double y1, double y2, int best, bool inside)
+{
+#pragma clang fp contract(off)
+    double d = 0.0;
+    if (inside) {
+        const double den = y0 - 2.0 * y1 + y2;
+        if (den < 0.0) {
+            d = 0.5 * (y0 - y2) / den;
+            d = d < -0.5 ? -0.5 : (d > 0.5 ? 0.5 : d);
+        }
+    }
+    return (double)best + d;
+}
+
 #define TDOA_MAX_PAIRS 28  // 8 mics
 #define TDOA_MAX_MICS_K 8
 #define TDOA_LS_ITERS 10   // least-squares refinement steps (tdoa_ls.hip)
@@ -91,6 +111,11 @@ struct tdoa_kout {
     int64_t *weighted;
     float *scores_f;
     float *weighted_f;
+    // per pair the raw scores at lags best - 1, best, best + 1 (the least-
+    // squares refinement's parabolic vertex, tdoa_ls.hip): [B][P][3]; written by
+    // the kernels that keep the scores on chip (k_frame16) instead of scores_f
+    // (slots outside the lag range are not written and not read)
+    float *peak3;
 };
 
 // Streaming state of one pipeline (tdoa_stream.hip); all device pointers.
@@ -139,7 +164,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
 bool tdoa_direct_fused_grid(const tdoa_kparams &kp);
 int tdoa_launch_heatmap(const tdoa_kparams &kp, const void *weighted, const void *max_L,
                         bool is_float, int64_t B, uint8_t *classes, void *stream);
-int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
+int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float, const float *peak3,
                    const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
                    int64_t B, void *stream);
 size_t tdoa_stream_trigger_lds(int M, int N, int H);
@@ -165,6 +190,8 @@ bool tdoa_gcc_phat_needs_split(int M, int N);
 void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
                          const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img);
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
+bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp);
+bool tdoa_gcc_phat_peak3(const tdoa_kparams &kp);
 int tdoa_launch_gcc_phat_split(const tdoa_kparams &kp, const tdoa_kout &out,
                                const int16_t *frames, int64_t B, float eps2_int16,
                                void *scratch, size_t scratch_bytes, void *stream);

@@ -20,20 +20,14 @@ template <typename T>
 __device__ __forceinline__ double ls_tau(const T *s, int K, int best)
 {
     const int S = K / 2, kb = best + S;
-    double d = 0.0;
-    if (kb > 0 && kb < K - 1) {
-        const double y0 = (double)s[kb - 1], y1 = (double)s[kb], y2 = (double)s[kb + 1];
-        const double den = y0 - 2.0 * y1 + y2;
-        if (den < 0.0) {
-            d = 0.5 * (y0 - y2) / den;
-            d = d < -0.5 ? -0.5 : (d > 0.5 ? 0.5 : d);
-        }
-    }
-    return (double)best + d;
+    const bool inside = kb > 0 && kb < K - 1;
+    return inside ? ls_tau3((double)s[kb - 1], (double)s[kb], (double)s[kb + 1], best, true)
+                  : ls_tau3(0.0, 0.0, 0.0, best, false);
 }
 
 template <typename T>
 __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict__ scores,
+                                            const float *__restrict__ peak3,
                                             const int32_t *__restrict__ lags,
                                             const int32_t *__restrict__ cells,
                                             float *__restrict__ xy_ls, float *__restrict__ rms_out,
@@ -44,8 +38,17 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
         return;
     const int M = kp.M, P = kp.P, K = kp.K;
     double tau[TDOA_MAX_PAIRS];
-    for (int p = 0; p < P; p++)
-        tau[p] = ls_tau(scores + ((size_t)f * P + p) * K, K, lags[f * P + p]);
+    for (int p = 0; p < P; p++) {  // the sub-sample lags: from the peaks' scores or the raw scores
+        const int best = lags[f * P + p];
+        if (peak3) {
+            const float *y = peak3 + ((size_t)f * P + p) * 3;
+            const bool inside = best + K / 2 > 0 && best + K / 2 < K - 1;
+            tau[p] = inside ? ls_tau3((double)y[0], (double)y[1], (double)y[2], best, true)
+                            : ls_tau3(0.0, 0.0, 0.0, best, false);
+        } else {
+            tau[p] = ls_tau(scores + ((size_t)f * P + p) * K, K, best);
+        }
+    }
     int cell = cells[f];
     cell = cell < 0 ? 0 : (cell >= kp.G ? kp.G - 1 : cell);
     const double sc = (double)kp.grid_scale;
@@ -103,7 +106,7 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
 
 }  // namespace
 
-int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
+int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float, const float *peak3,
                    const int32_t *lags, const int32_t *cells, float *xy_ls, float *rms,
                    int64_t B, void *stream)
 {
@@ -112,13 +115,15 @@ int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float,
     const int64_t grid = (B + 127) / 128;
     if (grid > 0x7fffffff)
         return tdoa_set_error(-1, "ls: batch too large for one launch");
+    if (!peak3 && !scores)
+        return tdoa_set_error(-1, "ls: neither peak scores nor raw scores");
     hipStream_t st = (hipStream_t)stream;
-    if (is_float)
+    if (is_float || peak3)
         hipLaunchKernelGGL(k_ls<float>, dim3((unsigned)grid), dim3(128), 0, st, kp,
-                           (const float *)scores, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
+                           (const float *)scores, peak3, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
     else
         hipLaunchKernelGGL(k_ls<int64_t>, dim3((unsigned)grid), dim3(128), 0, st, kp,
-                           (const int64_t *)scores, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
+                           (const int64_t *)scores, peak3, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char buf[256];

@@ -274,7 +274,8 @@ __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)
             const uint32_t d = (w[t] | 0x01000100u) - off2;
             const float s0 = (float)(int8_t)(d & 0xFFu);
             const float s1 = (float)(int8_t)((d >> 16) & 0xFFu);
-            v[t] = f2{floorf(s0 * wf.x), floorf(s1 * wf.y)};
+            const f2 pr = f2{s0, s1} * wf;  // one packed multiply
+            v[t] = f2{floorf(pr.x), floorf(pr.y)};
         }
     }
     after_front();  // the row's words are consumed
@@ -701,15 +702,28 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             consume(gn, u0 + 256);
         }
         LEAN_MARK();
+        // each lane requests the first cell of its own candidate before the
+        // wave reduction: the winner's comes back by a lane read, not by a
+        // dependent load after it
+        int mycell[2], myu[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            myu[j] = gu[j];
+            mycell[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
+        }
 #pragma unroll
         for (int j = 0; j < 2; j++)
             wave_argmax_to63(gv[j], gu[j]);
         LEAN_MARK();
-        if (lane64 == 63) {
-            int cells[2];
+        int wcell[2];
 #pragma unroll
-            for (int j = 0; j < 2; j++)  // every L compared false (NaN scores): tuple 0
-                cells[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
+        for (int j = 0; j < 2; j++) {
+            const int fu = __builtin_amdgcn_readlane(gu[j], 63);
+            const uint64_t wm = __ballot(myu[j] == fu && fu >= 0 && fu < kp.U);
+            wcell[j] = wm ? __builtin_amdgcn_readlane(mycell[j], __builtin_ctzll(wm)) : kp.tuple_cell[0];
+        }
+        if (lane64 == 63) {
+            const int cells[2] = {wcell[0], wcell[1]};  // no winner (NaN scores): tuple 0
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const int64_t fs = base + 2 * wave + j;

@@ -466,11 +466,13 @@ __device__ __forceinline__ void static_for(F &&f)
 }
 
 #ifdef TDOA_DIAG
-// diagnostic build only: s_memtime per phase boundary, per wave of the first 256 frames
+// diagnostic build only: s_memtime per phase boundary (32 per wave: stamps
+// 0..28, [29] end of the first frame, [30] / [31] realtime start / end), per
+// wave of the first 128 workgroups
 __device__ unsigned long long g_diag_f16[1 << 16];
 #define F16_MARK()                                       \
     do {                                                 \
-        if (nst < 14)                                    \
+        if (nst < 29)                                    \
             stamp[nst++] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
@@ -478,6 +480,31 @@ __device__ unsigned long long g_diag_f16[1 << 16];
     do {           \
     } while (0)
 #endif
+
+// LDS bytes of k_frame16
+template <int C>
+constexpr size_t frame16_lds_base()
+{
+    constexpr int G = 16384 / C, BUF = C + C / 16;
+    return (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
+           3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2);
+}
+
+// The output block read through an opaque kernarg pointer: loads used once
+// per frame (the least-squares lags) stay where they are used instead of being
+// hoisted out of the frame loop and held in scalar registers across the
+// transforms.  kp and out are the kernel's first two arguments (kernarg
+// offsets 0 and sizeof(kp) rounded to 8).
+__device__ __forceinline__ const char *kernarg_base()
+{
+    const char *k = (const char *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return k;
+}
+__device__ __forceinline__ const tdoa_kout *kernarg_out()
+{
+    return reinterpret_cast<const tdoa_kout *>(kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
+}
 
 template <int C, int M>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
@@ -520,9 +547,9 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
     const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
 #ifdef TDOA_DIAG
-    unsigned long long stamp[16] = {};
+    unsigned long long stamp[32] = {};
     int nst = 0;
-    stamp[14] = __builtin_amdgcn_s_memrealtime();
+    stamp[30] = __builtin_amdgcn_s_memrealtime();
 #endif
     // persistent over frames (one workgroup per CU): the next frame's words are
     // requested when the pair rounds start, so their HBM latency hides behind
@@ -795,17 +822,28 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const size_t gb = (size_t)(fr * P + p) * K;
             if (oka) {
                 const int dd = ka > bk ? ka - bk : bk - ka;
+                const float wa = sa * priorl[dd];
                 if (out.scores_f)
                     out.scores_f[gb + ka] = sa;
                 if (out.weighted_f)
-                    out.weighted_f[gb + ka] = sa * priorl[dd];
+                    out.weighted_f[gb + ka] = wa;
             }
             if (okb) {
                 const int dd = kb > bk ? kb - bk : bk - kb;
+                const float wb = sb * priorl[dd];
                 if (out.scores_f)
                     out.scores_f[gb + kb] = sb;
                 if (out.weighted_f)
-                    out.weighted_f[gb + kb] = sb * priorl[dd];
+                    out.weighted_f[gb + kb] = wb;
+            }
+            if (float *pk3 = kernarg_out()->peak3) {
+                // the least-squares refinement's raw scores around the peak:
+                // the lanes holding lags bk - 1 .. bk + 1 store them
+                float *dst = pk3 + (size_t)(fr * P + p) * 3 + 1 - bk;
+                if (oka && ka >= bk - 1 && ka <= bk + 1)
+                    dst[ka] = sa;
+                if (okb && kb >= bk - 1 && kb <= bk + 1)
+                    dst[kb] = sb;
             }
             if (l == 0) {
                 out.lags[fr * P + p] = bk - S;
@@ -824,15 +862,15 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 #ifdef TDOA_DIAG
     if (fr == blockIdx.x) {
-        stamp[15] = __builtin_amdgcn_s_memrealtime();
-        stamp[13] = __builtin_amdgcn_s_memtime();
+        stamp[31] = __builtin_amdgcn_s_memrealtime();
+        stamp[29] = __builtin_amdgcn_s_memtime();
     }
 #endif
     }  // frames
 #ifdef TDOA_DIAG
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)
-        for (int i = 0; i < 16; i++)
-            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + i] = stamp[i];
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 128)
+        for (int i = 0; i < 32; i++)
+            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + i] = stamp[i];
 #endif
 }
 #undef F16_MARK
@@ -841,17 +879,14 @@ template <int C, int M>
 int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                    float e2, hipStream_t st)
 {
-    constexpr int G = 16384 / C, BUF = C + C / 16;
-    const size_t lds = (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
-                       3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2);
     if (B <= 0)
         return 0;
+    const size_t lds = frame16_lds_base<C>();
     const int res = tdoa_resident_blocks((const void *)k_frame16<C, M>, 1024, lds);
     if (res < 1)
         return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
     const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
-    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B,
-                       e2);
+    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];
@@ -859,6 +894,12 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
         return tdoa_set_error(-2, msg);
     }
     return 0;
+}
+
+// the fused per-frame kernel's shapes (one group of threads per mic)
+bool frame16_shape(const tdoa_kparams &kp)
+{
+    return (kp.N == 4096 && (kp.M == 3 || kp.M == 4)) || (kp.N == 2048 && (kp.M == 4 || kp.M == 8));
 }
 
 __global__ void k_r16_gate(const int32_t *__restrict__ lags, uint8_t *__restrict__ gate, int64_t B, int P)
@@ -912,6 +953,12 @@ int launch_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *fram
 bool tdoa_phat_r16_fits(int M, int N, int S)
 {
     return (N == 2048 || N == 4096) && M >= 2 && M <= TDOA_MAX_MICS_K && S <= 63;
+}
+
+// the least-squares refinement's peak scores come from the kernel (peak3)
+bool tdoa_phat_r16_peak3(const tdoa_kparams &kp)
+{
+    return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) && frame16_shape(kp);
 }
 
 int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,

@@ -265,19 +265,19 @@ def test_grid_bb_exact_on_own_scores(shape, kind):
 # scores of correlations.c:20-33).  The two engines score lags differently
 # (PHAT-whitened fp32 vs raw integer products), so their grid maxima can fall
 # on different cells where DIRECT's own L is nearly flat.  Contract per shape,
-# on ADC-like integer-delay frames (synth.adc_frames):
-#   agreement rate >= CELL_AGREE[shape]  (the measured rate minus a slack)
-#   every disagreeing frame: GCC's cell is a near-maximum of DIRECT's own L
-#     ((max L - L[gcc cell]) / |max L| <= CELL_L_GAP) or lies within
-#     CELL_RADIUS grid cells (Chebyshev) of DIRECT's cell
+# on ADC-like integer-delay frames (synth.adc_frames, the bench's seeds):
+#   agreement rate >= CELL_AGREE[shape]: measured 0.9995 (cfg2, 4096 frames),
+#     0.9644 (cfg3, 2048), 0.9453 (cfg4, 2048), minus a 0.001-0.01 slack
+#   every disagreeing frame is a near-tie of DIRECT's own L: (max L - L[gcc
+#     cell]) / |max L| <= CELL_L_GAP (measured max 0.0066; median 0.0009-0.0033),
+#     the cells lying 1-2 grid cells apart at the median (max 7)
 CELL_SHAPES = {
     "cfg2": dict(M=3, N=1024, mics=None, B=4096),
     "cfg3": dict(M=4, N=4096, mics="square", B=2048),
     "cfg4": dict(M=8, N=2048, mics="circle", B=2048),
 }
-CELL_AGREE = {"cfg2": 0.995, "cfg3": 0.94, "cfg4": 0.92}
-CELL_L_GAP = 0.05
-CELL_RADIUS = 3
+CELL_AGREE = {"cfg2": 0.9985, "cfg3": 0.955, "cfg4": 0.935}
+CELL_L_GAP = 0.01
 
 
 def _direct_L_at(weighted, lut, cells):
@@ -306,7 +306,7 @@ def test_cell_contract_vs_direct(shape):
     gap = (d["max_L"] - L_gcc) / np.maximum(np.abs(d["max_L"]), 1)
     W = 101
     cheb = np.maximum(np.abs(got["cell"] % W - d["cell"] % W), np.abs(got["cell"] // W - d["cell"] // W))
-    bad = ~same & ~(gap <= CELL_L_GAP) & ~(cheb <= CELL_RADIUS)
+    bad = ~same & ~(gap <= CELL_L_GAP)
     print(f"{shape}: cells equal {rate:.4f}; disagreements {int((~same).sum())}: "
           f"L gap p50 {np.median(gap[~same]) if (~same).any() else 0:.4f} max {gap.max():.4f}, "
           f"cells apart p50 {np.median(cheb[~same]) if (~same).any() else 0} max {cheb.max()}")

@@ -2,7 +2,7 @@
 """Phase timeline of k_frame16 (the fused long-frame GCC-PHAT kernel) from
 libtdoa_diag.so's per-wave s_memtime stamps.  Diagnostic only.
 
-    TDOA_PHAT_FUSED=1 python tools/diag_frame16.py [config 3|4] [B]
+    python tools/diag_frame16.py [config 3|4] [B]
 """
 import ctypes as C
 import os
@@ -10,7 +10,6 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault("TDOA_LIB", os.path.join(ROOT, "audio-triangulation_amd", "tdoa", "libtdoa_diag.so"))
-os.environ.setdefault("TDOA_PHAT_FUSED", "1")
 sys.path.insert(0, os.path.join(ROOT, "audio-triangulation_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -32,7 +31,7 @@ L = tdoa.load()
 L.tdoa_diag_fetch_f16.argtypes = [C.c_void_p, C.c_int]
 buf = np.zeros(1 << 16, np.uint64)
 assert L.tdoa_diag_fetch_f16(buf.ctypes.data_as(C.c_void_p), 1 << 16) == 0
-st = buf.reshape(-1, 16).astype(np.int64)
+st = buf.reshape(-1, 32).astype(np.int64)
 st = st[st[:, 0] > 0]
 G = 16384 // N
 P = M * (M - 1) // 2
@@ -40,12 +39,12 @@ R = (P + G - 1) // G
 names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} inv"] for r in range(R)], [])
 n = len(names)
 print(f"config {cfg}: M={M} N={N} P={P} G={G} rounds={R}, waves {len(st)}")
-life = st[:, 13] - st[:, 0]
+life = st[:, 29] - st[:, 0]
 print("wave life (cycles): p50 %.0f; clock %.2f GHz" % (np.median(life),
-      np.median(life / ((st[:, 15] - st[:, 14]) / 100e6)) / 1e9))
+      np.median(life / ((st[:, 31] - st[:, 30]) / 100e6)) / 1e9))
 print("phase durations (cycles): p10 / p50 / p90")
 for i in range(1, n):
     d = st[:, i] - st[:, i - 1]
     print(f"  {names[i]:9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
-d = st[:, 13] - st[:, n - 1]
+d = st[:, 29] - st[:, n - 1]
 print(f"  {'tail':9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
