@@ -384,7 +384,8 @@ __device__ __forceinline__ void store_max(const tdoa_kout &o, int64_t i, float v
 template <typename T, int FMAX = TDOA_FMAX, int TWC = (TDOA_MAX_PAIRS + 3) / 4>
 __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, int *redi,
                              const tdoa_kout &out, int64_t f0, int nf,
-                             const uint32_t *tuples = nullptr, const int32_t *cells = nullptr)
+                             const uint32_t *tuples = nullptr, const int32_t *cells = nullptr,
+                             uint32_t omask = 0xFFFFFFFFu)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
     const int nt = blockDim.x;
@@ -455,7 +456,7 @@ __device__ void grid_phase_t(const tdoa_kparams &kp, const T *scores, T *redv, i
     }
     __syncthreads();
     TDOA_GRID_MARK(9);
-    if (tid < nf) {
+    if (tid < nf && ((omask >> tid) & 1u)) {  // omask: the frames whose outputs are written
         const int f = tid;
         T v = redv[f];
         int ui = redi[f];

@@ -170,7 +170,8 @@ __device__ void argmax_prior_mf(const tdoa_kparams &kp, int64_t *scores, int *be
 // thread's tuples, the wave (DPP) and the workgroup (LDS, one barrier)
 template <int GR>
 __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t *red, const uint32_t (&q)[GR],
-                        const int32_t (&cl)[GR], const tdoa_kout &out, int64_t f0, int nf)
+                        const int32_t (&cl)[GR], const tdoa_kout &out, int64_t f0, int nf,
+                        uint32_t omask = 0xFFFFFFFFu)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6, nt = blockDim.x;
     const int K = kp.K, P = kp.P, U = kp.U;
@@ -205,7 +206,7 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
             red[wave * 4 + f] = best[f];
     __syncthreads();
     TDOA_GRID_MARK(9);
-    if (tid < nf) {
+    if (tid < nf && ((omask >> tid) & 1u)) {  // omask: the frames whose outputs are written
         const int f = tid;
         uint64_t k = red[f];
         for (int w = 1; w < nwaves; w++) {
@@ -223,6 +224,122 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
             out.xy[2 * fi] = (float)(cx - kp.half_w) / kp.grid_scale;
             out.xy[2 * fi + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
         }
+    }
+}
+
+// Streaming (tdoa_stream.cpp, BASELINE config 5): the EMA of correlations.c:
+// 38-63 on the stream state of the batch's gated frames (sample_compute.h:134),
+// on the weighted scores still in LDS -- which then hold the EMA scores the
+// grid solve runs on (vga_heatmap.h reads corr_*) -- and the EMA argmax per
+// pair (ema_best).  The clock now = end * 10^6 / fs.  Replaces k_stream_update's
+// per-slot pass for the shapes this kernel solves (no fresh-score round trip).
+// The stream states are requested at the kernel's start (ema_prefetch: the
+// thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
+// latency hides behind the staging and the xcorr.
+constexpr int EMA_E = 2;  // state elements per thread: F P K <= EMA_E x threads (host-checked)
+
+struct EmaPre {
+    int64_t ev[EMA_E];
+};
+
+__device__ __forceinline__ EmaPre ema_prefetch(const tdoa_kparams &kp, const tdoa_stream_params &sp,
+                                               int64_t f0, int nf)
+{
+    EmaPre e;
+    const int PK = kp.P * kp.K;
+#pragma unroll
+    for (int i = 0; i < EMA_E; i++) {
+        const int x = (int)threadIdx.x + i * (int)blockDim.x;
+        const int f = x / PK;
+        e.ev[i] = f < nf ? sp.est[(size_t)sp.ids[f0 + f] * PK + (x - f * PK)] : 0;
+    }
+    return e;
+}
+
+template <bool IL>
+__device__ uint32_t ema_mf(const tdoa_kparams &kp, const tdoa_stream_fuse &ef, const EmaPre &pre,
+                           int64_t *scores, const int *bestlag, float *decl, int64_t f0, int nf)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const int K = kp.K, P = kp.P, PK = P * K;
+    const tdoa_stream_params &sp = ef.sp;
+    uint32_t gmask = 0;
+    for (int f = 0; f < nf; f++) {  // sum_p best^2 > 4 (sample_compute.h:124-134)
+        int tot = 0;
+        for (int q = 0; q < P; q++) {
+            const int b = bestlag[f * P + q];
+            tot += b * b;
+        }
+        gmask |= (tot > 4 ? 1u : 0u) << f;
+    }
+    uint64_t now = 0;
+    int s = 0;
+    if (tid < nf) {  // the frame's decay (correlations.c:40-43), shared through LDS
+        const int64_t slot = f0 + tid;
+        s = sp.ids[slot];
+        now = (uint64_t)sp.end[slot] * 1000000u / (uint64_t)sp.fs;
+        decl[tid] = tdoa_decay_dev(now, sp.last[s]);
+    }
+    __syncthreads();
+    // the EMA, element by element, of the states requested at the start
+#pragma unroll
+    for (int i = 0; i < EMA_E; i++) {
+        const int x = tid + i * (int)blockDim.x;
+        const int f = x / PK;
+        if (f < nf && ((gmask >> f) & 1u)) {
+            const int p = (x - f * PK) / K, k = x - f * PK - p * K;
+            int64_t *sc = scores + sidx<IL>(f, p, k, P, K);
+            const int64_t ev = pre.ev[i];
+            const float delta = (float)(*sc - ev) * decl[f];
+            const float sum = (float)ev + delta;
+            const int64_t nv = (int64_t)sum;
+            sp.est[(size_t)sp.ids[f0 + f] * PK + (x - f * PK)] = nv;
+            *sc = nv;
+        }
+    }
+    __syncthreads();  // EMA scores in LDS
+    if (ef.so.ema_best) {
+        constexpr int KS = IL ? 4 : 1;
+        for (int fp = wave; fp < nf * P; fp += nwaves) {
+            const int f = fp / P, p = fp - f * P;
+            if (!((gmask >> f) & 1u))
+                continue;
+            const int64_t *sc = scores + sidx<IL>(f, p, 0, P, K);
+            uint64_t key = 0;
+            for (int k = lane; k < K; k += 64) {
+                const uint64_t kk = vkey<7>(sc[KS * k], k);  // |EMA| <= 2^42 < 2^47 (tdoa_keys.h)
+                key = kk > key ? kk : key;
+            }
+            const int bk = key_index<7>(lane63_u64(wave_umax_dpp(key)));
+            if (lane == 0)
+                ef.so.ema_best[(f0 + f) * P + p] = bk - kp.S;
+        }
+    }
+    if (tid < nf) {
+        const int64_t slot = f0 + tid;
+        if ((gmask >> tid) & 1u)
+            sp.last[s] = now;
+        else if (ef.so.cell)
+            ef.so.cell[slot] = -1;  // not gated: no update, no solve (sample_compute.h:134)
+        if (ef.so.stream_id)
+            ef.so.stream_id[slot] = s;
+        if (ef.so.end)
+            ef.so.end[slot] = sp.end[slot];
+    }
+    if (tid == 0 && gmask)
+        atomicAdd((unsigned long long *)&sp.stats[1], (unsigned long long)__builtin_popcount(gmask));
+    return gmask;
+}
+
+// the hop's bookkeeping (k_stream_update's block 0): the device sample clock,
+// the running trigger count, the hop's trigger count
+__device__ __forceinline__ void ema_hop(const tdoa_stream_fuse &ef, int cnt)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *ef.sp.pos += ef.sp.H;  // the trigger kernel has read it
+        ef.sp.stats[0] += cnt;
+        if (ef.so.count)
+            *ef.so.count = cnt;
     }
 }
 
@@ -356,17 +473,19 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
     __syncthreads();
 }
 
-template <bool PREPARED, int TWC, int CH>
-__global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
+template <bool PREPARED, int TWC, int CH, bool EMA>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA && CH <= 4 ? 6 : 1))) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
                                                       const int16_t *__restrict__ frames, int64_t B,
                                                       const int32_t *__restrict__ count, int n0, int nq,
-                                                      MfTabs tb)
+                                                      MfTabs tb, tdoa_stream_fuse ef)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
     if (count) {  // batch size known on the device only (streaming pipeline)
         const int64_t c = *count;
+        if constexpr (EMA)
+            ema_hop(ef, (int)c);
         B = c < B ? c : B;
         if (f0 >= B)
             return;
@@ -388,6 +507,9 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
             gc[r] = do_grid && u < kp.U ? kp.tuple_cell[u] : 0;
         }
     }
+    EmaPre epre{};
+    if constexpr (EMA)
+        epre = ema_prefetch(kp, ef.sp, f0, nf);
     stage_mf<PREPARED, CH>(kp, sm, smem, tb, frames, f0, nf);
     DIAG_STAMP(1);
     DIAG_STAMP(2);
@@ -453,13 +575,19 @@ __global__ void __launch_bounds__(1024) k_direct_mfma(tdoa_kparams kp, tdoa_kout
     DIAG_STAMP(3);
     argmax_prior_mf<KEYGRID>(kp, sm.scores, sm.best, reinterpret_cast<const float *>(smem + tb.prior), out, f0, nf);
     DIAG_STAMP(4);
+    // streaming: the EMA of the gated frames replaces their scores in LDS, and
+    // only gated frames are solved
+    uint32_t omask = 0xFFFFFFFFu;
+    if constexpr (EMA)
+        omask = ema_mf<KEYGRID>(kp, ef, epre, sm.scores, sm.best,
+                                reinterpret_cast<float *>(smem + tb.red + 16 * 4 * 8), f0, nf);
     // grid solve (vga_heatmap.h:99-108) on the weighted scores still in LDS:
     // no [B][P][K] round trip through HBM and no second launch
     if (do_grid) {
         if constexpr (KEYGRID)
-            grid_mf<GR>(kp, sm.scores, reinterpret_cast<uint64_t *>(smem + tb.red), gq, gc, out, f0, nf);
+            grid_mf<GR>(kp, sm.scores, reinterpret_cast<uint64_t *>(smem + tb.red), gq, gc, out, f0, nf, omask);
         else
-            grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf);
+            grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf, nullptr, nullptr, omask);
     }
     DIAG_STAMP(5);
 }
@@ -669,9 +797,20 @@ bool tdoa_direct_fused_grid(const tdoa_kparams &kp)
     return chunks <= 8;
 }
 
+// ... and can also run the streaming EMA (k_direct_mfma<.., EMA>): the
+// workgroup's stream states fit its prefetch registers
+bool tdoa_direct_ema_fits(const tdoa_kparams &kp)
+{
+    if (!tdoa_direct_fused_grid(kp))
+        return false;
+    int F, threads, chunks;
+    mf_shape(kp, F, threads, chunks);
+    return F * kp.P * kp.K <= EMA_E * threads;
+}
+
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
                        int64_t B, bool prepared, void *stream, int *lds_bytes_out,
-                       const int32_t *count_dev)
+                       const int32_t *count_dev, const tdoa_stream_fuse *ema)
 {
     if (((uintptr_t)frames & 15) != 0)
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
@@ -690,7 +829,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         tb.prior = (int)o;
         o += (size_t)128 * 4;
         tb.red = (int)o;
-        o += (size_t)16 * 4 * 8;
+        o += (size_t)16 * 4 * 8 + 16 * 4;  // + the EMA's per-frame decay (ema_mf)
         // the keyed grid (TWC = 1): single-word tuples, <= 4 per thread held in
         // registers, the score table frame-interleaved for four frames, cells in
         // the key's 16 index bits; other shapes (wide geometries with more
@@ -706,9 +845,20 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
             return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
         hipStream_t st = (hipStream_t)stream;
         constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
-#define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                  \
-    hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH>), dim3((unsigned)grid), dim3(threads), lds, st, kp, \
-                       out, frames, B, count_dev, n0, nq, tb)
+        const tdoa_stream_fuse ef = ema ? *ema : tdoa_stream_fuse{};
+        if (ema && (!count_dev || prepared))
+            return tdoa_set_error(-1, "DIRECT: the EMA launch takes a device-sized batch of raw frames");
+        if (ema && kp.F * kp.P * kp.K > EMA_E * threads)
+            return tdoa_set_error(-1, "DIRECT: EMA state of a workgroup exceeds its prefetch registers");
+#define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                          \
+    do {                                                                                                       \
+        if (ema)                                                                                               \
+            hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH, !PREP>), dim3((unsigned)grid), dim3(threads), lds, \
+                               st, kp, out, frames, B, count_dev, n0, nq, tb, ef);                             \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH, false>), dim3((unsigned)grid), dim3(threads),     \
+                               lds, st, kp, out, frames, B, count_dev, n0, nq, tb, ef);                        \
+    } while (0)
 #define TDOA_LAUNCH_MF_CH(PREP, TWC)      \
     do {                                  \
         if (chunks <= 2)                  \

@@ -43,6 +43,16 @@ __device__ __forceinline__ double ls_tau3(double y0, double y1, double y2, int b
     return (double)best + d;
 }
 
+// correlations.c:40-43: the EMA decay from the stream clock, in the
+// reference's float / double steps (no contraction whatever the TU's flags)
+__device__ __forceinline__ float tdoa_decay_dev(uint64_t now, uint64_t last)
+{
+#pragma clang fp contract(off)
+    const float dt = (float)(now - last) / 1e6f;
+    const float arg = -dt / 0.5f;
+    return (float)(1.0 - exp((double)arg));
+}
+
 #define TDOA_MAX_PAIRS 28  // 8 mics
 #define TDOA_MAX_MICS_K 8
 #define TDOA_LS_ITERS 10   // least-squares refinement steps (tdoa_ls.hip)
@@ -156,12 +166,20 @@ int tdoa_resident_blocks(const void *kernel, int threads, size_t lds);
 
 // Host-side launchers implemented in the .hip files.
 // count_dev (optional): device int32 batch size, B then only bounds the grid.
+// ema (optional, streaming): the launch also runs the EMA of the gated frames
+// and the grid on the EMA scores (k_direct_mfma only: tdoa_direct_fused_grid)
+struct tdoa_stream_fuse {
+    tdoa_stream_params sp;
+    tdoa_stream_kout so;
+};
 int tdoa_launch_direct(const tdoa_kparams &kp, const tdoa_kout &out,
                        const int16_t *frames, int64_t B, bool prepared,
                        void *stream, int *lds_bytes_out,
-                       const int32_t *count_dev = nullptr);
+                       const int32_t *count_dev = nullptr, const tdoa_stream_fuse *ema = nullptr);
 // the DIRECT launch for this shape also solves the grid (k_direct_mfma)
 bool tdoa_direct_fused_grid(const tdoa_kparams &kp);
+// ... and can also run the streaming EMA (tdoa_stream_fuse)
+bool tdoa_direct_ema_fits(const tdoa_kparams &kp);
 int tdoa_launch_heatmap(const tdoa_kparams &kp, const void *weighted, const void *max_L,
                         bool is_float, int64_t B, uint8_t *classes, void *stream);
 int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float, const float *peak3,

@@ -1,7 +1,8 @@
 // tdoa_stream.cpp -- host side of the streaming pipeline (include/tdoa.h,
 // kernels in tdoa_stream.hip): device state, the per-hop kernel sequence
-//   memset(count) -> k_stream_trigger -> k_direct (device-sized batch) -> k_stream_update
-// and its hipGraph capture / replay.
+//   memset(count) -> k_stream_trigger -> k_direct_mfma (device-sized batch,
+//   EMA + grid on the EMA scores fused) -- or, for shapes that kernel does not
+//   solve, k_direct -> k_stream_update -- and its hipGraph capture / replay.
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -78,12 +79,26 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
     int rc = tdoa_launch_stream_trigger(sp, st->S, s, &by_id);
     if (rc)
         return rc;
+    tdoa_kparams kp = st->kp;
+    kp.frame_ids = by_id ? sp.ids : nullptr;
+    if (tdoa_direct_ema_fits(kp)) {
+        // k_direct_mfma runs the EMA and the grid on the EMA scores itself:
+        // results straight into the caller's slots, no fresh-score round trip
+        tdoa_stream_fuse ef{};
+        ef.sp = sp;
+        ef.so = to_kout(out);
+        tdoa_kout ko{};
+        ko.lags = ef.so.lags ? ef.so.lags : sp.fresh_lags;
+        ko.gate = ef.so.gate;
+        ko.cell = ef.so.cell;
+        ko.xy = ef.so.xy;
+        ko.max_L = ef.so.max_L;
+        return tdoa_launch_direct(kp, ko, sp.frames, st->S, false, s, nullptr, sp.count, &ef);
+    }
     tdoa_kout ko{};
     ko.lags = sp.fresh_lags;
     ko.gate = sp.fresh_gate;
     ko.weighted = sp.fresh;
-    tdoa_kparams kp = st->kp;
-    kp.frame_ids = by_id ? sp.ids : nullptr;
     rc = tdoa_launch_direct(kp, ko, sp.frames, st->S, false, s, nullptr, sp.count);
     if (rc)
         return rc;

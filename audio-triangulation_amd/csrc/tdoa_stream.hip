@@ -456,12 +456,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
 }
 
 // correlations.c:40-43 in the reference's float/double steps
-__device__ __forceinline__ float decay_us(uint64_t now, uint64_t last)
-{
-    const float dt = (float)(now - last) / 1e6f;
-    const float arg = -dt / 0.5f;
-    return (float)(1.0 - exp((double)arg));
-}
+__device__ __forceinline__ float decay_us(uint64_t now, uint64_t last) { return tdoa_decay_dev(now, last); }
 
 __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, tdoa_kparams kp,
                                                        tdoa_stream_kout out)
