@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -103,6 +105,58 @@ __device__ __forceinline__ void half_argmax_to31(float &v, int &i)
 {
     row_argmax(v, i);
     dpp_argmax<0x142, 0xA>(v, i);
+}
+
+// ---- (max, first index) by keys: a float as a signed-int key with the same
+// order (-0.0 folded to +0.0 first, so equal floats give equal keys; no NaN
+// reaches these), reduced by DPP-fused v_max_i32 / v_min_i32 within rows and
+// v_permlane16/32_swap across rows; then the smallest index among the lanes
+// holding the maximum.  Every lane of the half-wave / wave receives both.
+__device__ __forceinline__ int fkey(float v)
+{
+    const int b = __builtin_bit_cast(int, v + 0.0f);
+    return b ^ ((b >> 31) & 0x7FFFFFFF);
+}
+__device__ __forceinline__ float fkey_value(int k) { return __builtin_bit_cast(float, k ^ ((k >> 31) & 0x7FFFFFFF)); }
+
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+template <bool MAX>
+__device__ __forceinline__ int row_reduce(int v)  // every lane of each 16-lane row
+{
+    auto op = [](int a, int b) { return MAX ? imax(a, b) : imin(a, b); };
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));   // xor 1
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));   // xor 2
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));  // half-row mirror
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));  // row mirror
+    return v;
+}
+template <bool MAX>
+__device__ __forceinline__ int half_reduce(int v)  // rows (0, 1) and (2, 3): each 32-lane half
+{
+    v = row_reduce<MAX>(v);
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return MAX ? imax(v, imax((int)r[0], (int)r[1])) : imin(v, imin((int)r[0], (int)r[1]));
+}
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce(int v)
+{
+    v = half_reduce<MAX>(v);
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return MAX ? imax(v, imax((int)r[0], (int)r[1])) : imin(v, imin((int)r[0], (int)r[1]));
+}
+// key: the lane's best key (INT_MIN: none), idx: its first index (INT_MAX: none)
+__device__ __forceinline__ void half_argmax_key(int &key, int &idx)
+{
+    const int mk = half_reduce<true>(key);
+    idx = half_reduce<false>(key == mk ? idx : INT_MAX);
+    key = mk;
+}
+__device__ __forceinline__ void wave_argmax_key(int &key, int &idx)
+{
+    const int mk = wave_reduce<true>(key);
+    idx = wave_reduce<false>(key == mk ? idx : INT_MAX);
+    key = mk;
 }
 
 }  // namespace

@@ -368,27 +368,6 @@ __device__ __forceinline__ int lane_res_sel(int l)
 }
 
 
-// max over each 32-lane half-wave, then both halves' results to every lane
-// (x: half-wave 0, y: half-wave 1) -- VALU/DPP only
-__device__ __forceinline__ f2 half_max2(float v)
-{
-    auto mx = [](float a, int b) { return fmaxf(a, __builtin_bit_cast(float, b)); };
-    int b = __builtin_bit_cast(int, v);
-    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, false));  // xor 1
-    b = __builtin_bit_cast(int, v);
-    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, false));  // xor 2
-    b = __builtin_bit_cast(int, v);
-    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x141, 0xF, 0xF, false));  // half-row mirror
-    b = __builtin_bit_cast(int, v);
-    v = mx(v, __builtin_amdgcn_mov_dpp(b, 0x140, 0xF, 0xF, false));  // row mirror
-    b = __builtin_bit_cast(int, v);
-    // row_bcast:15 into rows 1 and 3 (old = own value elsewhere)
-    v = mx(v, __builtin_amdgcn_update_dpp(b, b, 0x142, 0xA, 0xF, false));
-    const int r = __builtin_bit_cast(int, v);
-    return f2{__builtin_bit_cast(float, __builtin_amdgcn_readlane(r, 31)),
-              __builtin_bit_cast(float, __builtin_amdgcn_readlane(r, 63))};
-}
-
 // the lane id through an opaque move: lane-dependent values derived from it
 // are computed where they are used instead of being hoisted to the kernel's
 // start and held in registers across every phase
@@ -544,17 +523,18 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             const int ck[4] = {lb + S, lb + 1 + S, la + S, la + 1 + S};
             const bool ok[4] = {lb >= -S, lb + 1 >= -S, la <= S, la + 1 <= S};
             const float cv[4] = {y31.x * invL, y31.y * invL, y0.x * invL, y0.y * invL};
-            float bv = -INFINITY;
-            int bk = INT_MAX;
+            // the lane's first maximum of its candidates (ascending lags), then
+            // the half-wave's (correlations.c:20-23 first max) by keys
+            int bkey = INT_MIN, bk = INT_MAX;
 #pragma unroll
-            for (int c = 0; c < 4; c++)
-                if (ok[c] && (cv[c] > bv || bk == INT_MAX)) {
-                    bv = cv[c];
+            for (int c = 0; c < 4; c++) {
+                const int kc = fkey(cv[c]);
+                if (ok[c] && kc > bkey) {
+                    bkey = kc;
                     bk = ck[c];
                 }
-            half_argmax_to31(bv, bk);
-            const int b0 = __builtin_amdgcn_readlane(bk, 31), b1 = __builtin_amdgcn_readlane(bk, 63);
-            bk = fhw ? b1 : b0;
+            }
+            half_argmax_key(bkey, bk);  // every lane of the half-wave
             bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
             best[p] = bk - S;
             const int64_t ff = base + 2 * ((ft >> 6) & 7) + fhw;
@@ -711,14 +691,20 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             myu[j] = gu[j];
             mycell[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
         }
+        // (max L, first tuple) over the wave by keys (gv is -inf, never NaN,
+        // where a lane had no L above it: those lanes keep gu = INT_MAX)
+        int gk[2];
 #pragma unroll
-        for (int j = 0; j < 2; j++)
-            wave_argmax_to63(gv[j], gu[j]);
+        for (int j = 0; j < 2; j++) {
+            gk[j] = fkey(gv[j]);
+            wave_argmax_key(gk[j], gu[j]);
+            gv[j] = fkey_value(gk[j]);
+        }
         LEAN_MARK();
         int wcell[2];
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-            const int fu = __builtin_amdgcn_readlane(gu[j], 63);
+            const int fu = gu[j];
             const uint64_t wm = __ballot(myu[j] == fu && fu >= 0 && fu < kp.U);
             wcell[j] = wm ? __builtin_amdgcn_readlane(mycell[j], __builtin_ctzll(wm)) : kp.tuple_cell[0];
         }

@@ -372,18 +372,17 @@ __global__ void __launch_bounds__(C / 16, 6) k_pair16(tdoa_kparams kp, tdoa_kout
     const int ka = 2 * n + S, kb = 2 * n + 1 + S;
     const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
     const float sa = y.x * invL, sb = y.y * invL;
-    float bv = -INFINITY;
-    int bk = INT_MAX;
+    // first maximum (the lowest lag wins ties), by keys to every lane
+    int bkey = INT_MIN, bk = INT_MAX;
     if (oka) {
-        bv = sa;
+        bkey = fkey(sa);
         bk = ka;
     }
-    if (okb && (sb > bv || bk == INT_MAX)) {
-        bv = sb;
+    if (okb && fkey(sb) > bkey) {
+        bkey = fkey(sb);
         bk = kb;
     }
-    wave_argmax_to63(bv, bk);  // first maximum: the lowest lag wins ties
-    bk = __builtin_amdgcn_readlane(bk, 63);
+    wave_argmax_key(bkey, bk);
     bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);  // NaN scores: keep the index in range
     const int64_t fg = f_begin + fl;
     const size_t gb = (size_t)(fg * P + p) * K;
@@ -806,18 +805,17 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
             const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
             const float sa = y.x * invL, sb = y.y * invL;
-            float bv = -INFINITY;
-            int bk = INT_MAX;
+            // first maximum (the lowest lag wins ties), by keys to every lane
+            int bkey = INT_MIN, bk = INT_MAX;
             if (oka) {
-                bv = sa;
+                bkey = fkey(sa);
                 bk = ka;
             }
-            if (okb && (sb > bv || bk == INT_MAX)) {
-                bv = sb;
+            if (okb && fkey(sb) > bkey) {
+                bkey = fkey(sb);
                 bk = kb;
             }
-            wave_argmax_to63(bv, bk);  // first maximum: the lowest lag wins ties
-            bk = __builtin_amdgcn_readlane(bk, 63);
+            wave_argmax_key(bkey, bk);
             bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
             const size_t gb = (size_t)(fr * P + p) * K;
             if (oka) {

@@ -50,17 +50,25 @@ absolute_time_t default_clock()
 absolute_time_t (*g_clock)(void) = default_clock;
 int g_device = 0;
 
-// One lazily created 2-mic context (pair = (buf_a, buf_b)) plus device
-// staging buffers; the reference's functions are single-threaded, guard anyway.
+// One lazily created 2-mic context (pair = (buf_a, buf_b)), its stream and
+// one block of pinned, device-mapped host memory the per-frame kernels read
+// and write directly: a call is a host copy in, one launch, one stream
+// synchronisation and a host copy out (no hipMemcpy round trips).  The
+// reference's functions are single-threaded; guard anyway.
+struct HostIO {
+    int16_t frames[2][TDOA_REF_BUFFER_SIZE];  // buffers a, b (16-B aligned rows)
+    int16_t ring[TDOA_REF_BUFFER_SIZE];
+    int64_t i64[4 * 128];                     // weighted / est / fresh
+    int64_t power;
+    int32_t i32[64];                          // best lags
+    float f32[64];                            // decay
+};
 struct RefState {
     std::mutex mu;
     std::atomic<bool> ready{false};  // published after the state below (double-checked init)
     tdoa_ctx *ctx = nullptr;
-    int16_t *d_frames = nullptr;   // [2][1024]
-    int16_t *d_ring = nullptr;     // [1024]
-    int64_t *d_i64 = nullptr;      // scores/weighted/est/fresh scratch
-    int32_t *d_i32 = nullptr;
-    float *d_f32 = nullptr;
+    hipStream_t st = nullptr;
+    HostIO *io = nullptr;          // pinned, mapped: host and kernels address it alike
     int16_t *d_window = nullptr;   // Q15 DPSS(1024, 2)
 } g_ref;
 
@@ -94,11 +102,11 @@ RefState &ref()
     cfg.grid_half_h = 0;
     if (tdoa_create(&cfg, g_device, &g_ref.ctx) != TDOA_OK)
         die("tdoa_create");
-    check(hipMalloc(&g_ref.d_frames, 2 * 1024 * sizeof(int16_t)), "hipMalloc");
-    check(hipMalloc(&g_ref.d_ring, 1024 * sizeof(int16_t)), "hipMalloc");
-    check(hipMalloc(&g_ref.d_i64, 4 * 128 * sizeof(int64_t)), "hipMalloc");
-    check(hipMalloc(&g_ref.d_i32, 64 * sizeof(int32_t)), "hipMalloc");
-    check(hipMalloc(&g_ref.d_f32, 64 * sizeof(float)), "hipMalloc");
+    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipStreamCreateWithFlags(&g_ref.st, hipStreamNonBlocking), "hipStreamCreate");
+    check(hipHostMalloc(reinterpret_cast<void **>(&g_ref.io), sizeof(HostIO),
+                        hipHostMallocMapped | hipHostMallocCoherent),
+          "hipHostMalloc");
     check(hipMalloc(&g_ref.d_window, 1024 * sizeof(int16_t)), "hipMalloc");
     int32_t w[1024];
     tdoa_get_window(g_ref.ctx, w);
@@ -110,25 +118,25 @@ RefState &ref()
     return g_ref;
 }
 
-// One op of k_ref_buffer on a single 1024-sample buffer.
+// One op of k_ref_buffer on a single 1024-sample buffer, in place in the
+// mapped host block
 void buffer_op(int op, struct buffer_t *dst, const struct rolling_buffer_t *ring)
 {
     RefState &R = ref();
     check(hipSetDevice(g_device), "hipSetDevice");
-    int16_t *d_buf = R.d_frames;
+    HostIO &io = *R.io;
+    int16_t *buf = io.frames[0];
     if (ring)
-        check(hipMemcpy(R.d_ring, ring->buffer, sizeof ring->buffer, hipMemcpyHostToDevice),
-              "hipMemcpy");
+        std::memcpy(io.ring, ring->buffer, sizeof ring->buffer);
     else
-        check(hipMemcpy(d_buf, dst->buffer, sizeof dst->buffer, hipMemcpyHostToDevice),
-              "hipMemcpy");
-    if (tdoa_launch_ref_buffer(op, d_buf, R.d_ring, ring ? ring->head : 0, R.d_i64, R.d_window,
-                               TDOA_REF_BUFFER_SIZE, nullptr) != 0)
+        std::memcpy(buf, dst->buffer, sizeof dst->buffer);
+    if (tdoa_launch_ref_buffer(op, buf, io.ring, ring ? ring->head : 0, &io.power, R.d_window,
+                               TDOA_REF_BUFFER_SIZE, R.st) != 0)
         die("k_ref_buffer");
-    check(hipMemcpy(dst->buffer, d_buf, sizeof dst->buffer, hipMemcpyDeviceToHost), "hipMemcpy");
+    check(hipStreamSynchronize(R.st), "hipStreamSynchronize");
+    std::memcpy(dst->buffer, buf, sizeof dst->buffer);
     if (op == 0)
-        check(hipMemcpy(&dst->power, R.d_i64, sizeof(int64_t), hipMemcpyDeviceToHost),
-              "hipMemcpy");
+        dst->power = io.power;
 }
 
 }  // namespace
@@ -217,21 +225,18 @@ extern "C" void correlations_init(struct correlations_t *corr, const struct buff
 {
     RefState &R = ref();
     check(hipSetDevice(g_device), "hipSetDevice");
-    check(hipMemcpy(R.d_frames, a->buffer, sizeof a->buffer, hipMemcpyHostToDevice), "hipMemcpy");
-    check(hipMemcpy(R.d_frames + TDOA_REF_BUFFER_SIZE, b->buffer, sizeof b->buffer,
-                    hipMemcpyHostToDevice),
-          "hipMemcpy");
+    HostIO &io = *R.io;
+    std::memcpy(io.frames[0], a->buffer, sizeof a->buffer);
+    std::memcpy(io.frames[1], b->buffer, sizeof b->buffer);
     tdoa_outputs o;
     std::memset(&o, 0, sizeof o);
-    o.lags = R.d_i32;
-    o.weighted = R.d_i64;
-    if (tdoa_correlate_prepared(R.ctx, R.d_frames, 1, &o, nullptr) != TDOA_OK)
+    o.lags = io.i32;
+    o.weighted = io.i64;
+    if (tdoa_correlate_prepared(R.ctx, &io.frames[0][0], 1, &o, R.st) != TDOA_OK)
         die("correlations_init");
-    check(hipMemcpy(corr->correlations, R.d_i64, sizeof corr->correlations, hipMemcpyDeviceToHost),
-          "hipMemcpy");
-    int32_t best = 0;
-    check(hipMemcpy(&best, R.d_i32, sizeof best, hipMemcpyDeviceToHost), "hipMemcpy");
-    corr->best_shift = best;
+    check(hipStreamSynchronize(R.st), "hipStreamSynchronize");
+    std::memcpy(corr->correlations, io.i64, sizeof corr->correlations);
+    corr->best_shift = io.i32[0];
     corr->last_update = g_clock();
 }
 
@@ -239,20 +244,16 @@ extern "C" void correlations_average(struct correlations_t *est, struct correlat
 {
     RefState &R = ref();
     check(hipSetDevice(g_device), "hipSetDevice");
+    HostIO &io = *R.io;
     const absolute_time_t now = g_clock();
-    const float decay = tdoa_decay_us(now, est->last_update);
-    int64_t *d_est = R.d_i64, *d_new = R.d_i64 + 128;
-    check(hipMemcpy(d_est, est->correlations, sizeof est->correlations, hipMemcpyHostToDevice),
-          "hipMemcpy");
-    check(hipMemcpy(d_new, fresh->correlations, sizeof fresh->correlations, hipMemcpyHostToDevice),
-          "hipMemcpy");
-    check(hipMemcpy(R.d_f32, &decay, sizeof decay, hipMemcpyHostToDevice), "hipMemcpy");
-    if (tdoa_average_batch(R.ctx, 1, d_est, d_new, R.d_f32, R.d_i32, nullptr, nullptr) != TDOA_OK)
+    int64_t *h_est = io.i64, *h_new = io.i64 + 128;
+    std::memcpy(h_est, est->correlations, sizeof est->correlations);
+    std::memcpy(h_new, fresh->correlations, sizeof fresh->correlations);
+    io.f32[0] = tdoa_decay_us(now, est->last_update);
+    if (tdoa_average_batch(R.ctx, 1, h_est, h_new, io.f32, io.i32, nullptr, R.st) != TDOA_OK)
         die("correlations_average");
-    check(hipMemcpy(est->correlations, d_est, sizeof est->correlations, hipMemcpyDeviceToHost),
-          "hipMemcpy");
-    int32_t best = 0;
-    check(hipMemcpy(&best, R.d_i32, sizeof best, hipMemcpyDeviceToHost), "hipMemcpy");
-    est->best_shift = best;
+    check(hipStreamSynchronize(R.st), "hipStreamSynchronize");
+    std::memcpy(est->correlations, h_est, sizeof est->correlations);
+    est->best_shift = io.i32[0];
     est->last_update = now;
 }
