@@ -22,6 +22,7 @@
 #include <climits>
 #include <cmath>
 
+#include "tdoa_fft32.h"
 #include "tdoa_internal.h"
 
 namespace tdoa_bb {
@@ -102,10 +103,17 @@ __device__ __forceinline__ void dpp_better(T &v, int &i)
 {
     better<T>(v, i, dpp_mov<CTRL, RM>(v), dpp_mov<CTRL, RM>(i));
 }
-// the wave's (max, first index) to every lane
+// the wave's (max, first index) to every lane (float: by keys, tdoa_fft32.h;
+// v is never NaN here)
 template <typename T>
 __device__ __forceinline__ void wave_best(T &v, int &i)
 {
+    if constexpr (sizeof(T) == 4) {
+        int k = fkey(v);
+        wave_argmax_key(k, i);
+        v = fkey_value(k);
+        return;
+    }
     dpp_better<0xB1, 0xF>(v, i);
     dpp_better<0x4E, 0xF>(v, i);
     dpp_better<0x141, 0xF>(v, i);
@@ -155,7 +163,9 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
     } else {
         // many pairs: per pair the 8-wide running maxima M8[k] = max w[k..k+7]
         // (clamped to K - 1); a range of width <= 16 is max(M8[lo],
-        // M8[max(lo, hi - 7)]) -- independent reads, not a dependent chain
+        // M8[max(lo, hi - 7)]) -- independent reads, not a dependent chain.
+        // (Four pairs' rows per sync measured no faster: the pass is bound
+        // by LDS issue, not by its round trips.)
         for (int p = 0; p < P; p++) {
             const T *w = Wl + p * K;
             wave_lds_sync();  // previous pair's M8 reads come first

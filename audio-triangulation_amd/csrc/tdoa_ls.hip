@@ -25,7 +25,9 @@ __device__ __forceinline__ double ls_tau(const T *s, int K, int best)
                   : ls_tau3(0.0, 0.0, 0.0, best, false);
 }
 
-template <typename T>
+// MM: the mic count at compile time, so the per-frame arrays (P sub-sample
+// lags, M distances and their derivatives) are registers, not scratch
+template <typename T, int MM>
 __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict__ scores,
                                             const float *__restrict__ peak3,
                                             const int32_t *__restrict__ lags,
@@ -36,8 +38,10 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= B)
         return;
-    const int M = kp.M, P = kp.P, K = kp.K;
-    double tau[TDOA_MAX_PAIRS];
+    constexpr int M = MM, P = MM * (MM - 1) / 2;
+    const int K = kp.K;
+    double tau[P];
+#pragma unroll
     for (int p = 0; p < P; p++) {  // the sub-sample lags: from the peaks' scores or the raw scores
         const int best = lags[f * P + p];
         if (peak3) {
@@ -65,7 +69,8 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
                      dzu = h * (-h * u / n3);
         const double dxv = h * (-u * v / n3), dyv = h * (1.0 / n - v * v / n3),
                      dzv = h * (-h * v / n3);
-        double d[TDOA_MAX_MICS_K], du[TDOA_MAX_MICS_K], dv[TDOA_MAX_MICS_K];
+        double d[M], du[M], dv[M];
+#pragma unroll
         for (int m = 0; m < M; m++) {
             const double ex = px - (double)kp.mic_xy[2 * m], ey = py - (double)kp.mic_xy[2 * m + 1],
                          ez = pz;
@@ -75,17 +80,20 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
         }
         double a11 = 0.0, a12 = 0.0, a22 = 0.0, g1 = 0.0, g2 = 0.0;
         ss = 0.0;
-        for (int p = 0; p < P; p++) {
-            const int i = kp.pair_i[p], j = kp.pair_j[p];
-            const double r = (d[j] - d[i]) * kf - tau[p];
-            const double ju = (du[j] - du[i]) * kf, jv = (dv[j] - dv[i]) * kf;
-            a11 += ju * ju;
-            a12 += ju * jv;
-            a22 += jv * jv;
-            g1 += ju * r;
-            g2 += jv * r;
-            ss += r * r;
-        }
+        int p = 0;  // pairs (i, j), i < j, in the context's (lexicographic) order
+#pragma unroll
+        for (int i = 0; i < M; i++)
+#pragma unroll
+            for (int j = i + 1; j < M; j++, p++) {
+                const double r = (d[j] - d[i]) * kf - tau[p];
+                const double ju = (du[j] - du[i]) * kf, jv = (dv[j] - dv[i]) * kf;
+                a11 += ju * ju;
+                a12 += ju * jv;
+                a22 += jv * jv;
+                g1 += ju * r;
+                g2 += jv * r;
+                ss += r * r;
+            }
         if (it == iters)
             break;
         const double lam = 1e-3 * (a11 + a22) + 1e-12;
@@ -118,12 +126,29 @@ int tdoa_launch_ls(const tdoa_kparams &kp, const void *scores, bool is_float, co
     if (!peak3 && !scores)
         return tdoa_set_error(-1, "ls: neither peak scores nor raw scores");
     hipStream_t st = (hipStream_t)stream;
-    if (is_float || peak3)
-        hipLaunchKernelGGL(k_ls<float>, dim3((unsigned)grid), dim3(128), 0, st, kp,
-                           (const float *)scores, peak3, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
-    else
-        hipLaunchKernelGGL(k_ls<int64_t>, dim3((unsigned)grid), dim3(128), 0, st, kp,
-                           (const int64_t *)scores, peak3, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS);
+    const bool flt = is_float || peak3;
+#define TDOA_LS_M(MM)                                                                                   \
+    case MM:                                                                                            \
+        if (flt)                                                                                        \
+            hipLaunchKernelGGL((k_ls<float, MM>), dim3((unsigned)grid), dim3(128), 0, st, kp,          \
+                               (const float *)scores, peak3, lags, cells, xy_ls, rms, B, TDOA_LS_ITERS); \
+        else                                                                                            \
+            hipLaunchKernelGGL((k_ls<int64_t, MM>), dim3((unsigned)grid), dim3(128), 0, st, kp,        \
+                               (const int64_t *)scores, peak3, lags, cells, xy_ls, rms, B,              \
+                               TDOA_LS_ITERS);                                                          \
+        break
+    switch (kp.M) {
+        TDOA_LS_M(2);
+        TDOA_LS_M(3);
+        TDOA_LS_M(4);
+        TDOA_LS_M(5);
+        TDOA_LS_M(6);
+        TDOA_LS_M(7);
+        TDOA_LS_M(8);
+    default:
+        return tdoa_set_error(-1, "ls: num_mics outside 2..8");
+    }
+#undef TDOA_LS_M
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char buf[256];

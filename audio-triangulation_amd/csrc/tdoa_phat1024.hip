@@ -542,13 +542,18 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             for (int c = 0; c < 4; c++) {
                 const int d = ck[c] > bk ? ck[c] - bk : bk - ck[c];
                 wv[p][c] = ok[c] ? cv[c] * prior[ok[c] ? d : 0] : 0.0f;
-                if (ff < B && ok[c]) {
-                    const size_t gb = (size_t)(ff * P + p) * K;
-                    if (out.scores_f)
-                        out.scores_f[gb + ck[c]] = cv[c];
-                    if (out.weighted_f)
-                        out.weighted_f[gb + ck[c]] = wv[p][c];
-                }
+            }
+            if (out.scores_f || out.weighted_f) {  // debug / parity outputs (uniform branch)
+                float *sr = out.scores_f ? out.scores_f + (size_t)(ff * P + p) * K : nullptr;
+                float *wr = out.weighted_f ? out.weighted_f + (size_t)(ff * P + p) * K : nullptr;
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    if (ff < B && ok[c]) {
+                        if (sr)
+                            sr[ck[c]] = cv[c];
+                        if (wr)
+                            wr[ck[c]] = wv[p][c];
+                    }
             }
             if (ff < B && (ft & 31) == 0)
                 out.lags[ff * P + p] = bk - S;

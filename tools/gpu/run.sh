@@ -6,8 +6,6 @@
 #   tools/gpu/run.sh STEP [STEP ...]
 #
 #   test[:FILES]          pytest -m gpu (FILES comma-separated, default tests/)
-#   ab[:V1,V2,..]         bench config 2 once per TDOA_PHAT1024_WAVES value
-#                         (8 = two-waves-per-SIMD kernel, 4 = one-wave kernel)
 #   bench[:CFG[:ENGINE]]  bench.py line -> gpurun_out/bench_cCFG_ENGINE.json
 #   kstats[:CFG[:ENGINE]] rocprofv3 --kernel-trace --stats of the bench
 #   pmc[:CFG[:ENGINE]]    FETCH_SIZE and WRITE_SIZE passes (one run each)
@@ -52,14 +50,6 @@ for step in "$@"; do
         rc=$?
         grep -E "passed|failed|error" "$OUT/pytest.log" | tail -3
         [ $rc -ne 0 ] && { tail -30 "$OUT/pytest.log"; exit $rc; }
-        ;;
-    ab)
-        vs=$(field "$step" 2 "8,4")
-        for w in ${vs//,/ }; do
-            TDOA_PHAT1024_WAVES=$w timeout -k 10 240 python bench.py --steps ${STEPS:-400} --no-cpu \
-                $BENCH_ARGS > "$OUT/ab_$w.log" 2>&1 || { echo "bench $w failed"; tail -5 "$OUT/ab_$w.log"; exit 21; }
-            tail -1 "$OUT/ab_$w.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('WAVES=$w value %.4g kernel_ms %.4f frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))"
-        done
         ;;
     ablib)
         # bench config 2 once per library variant (audio-triangulation_amd/tdoa/<name>.so)
