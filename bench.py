@@ -528,10 +528,13 @@ def stream_traffic(args):
     except (OSError, ValueError):
         return None, None
     ks = e.get("kernels", {})
+    # k_stream_update runs only for shapes k_direct_mfma does not solve (the
+    # config-5 hop fuses the EMA and its grid into k_direct_mfma)
     names = ("k_stream_trigger_p", "k_direct_mfma", "k_stream_update")
     per = [sum(v["hbm_bytes"] for k, v in ks.items() if k.split("<")[0] == n) for n in names]
-    if not all(per):
+    if not all(per[:2]):
         return None, None
+    names = names if per[2] else names[:2]
     return sum(per), (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / "
                       f"WRITE_SIZE passes on {' + '.join(names)} ({e.get('date', 'undated')}), "
                       "read = 2 x FETCH_SIZE; the trigger re-reads the two previous hops")

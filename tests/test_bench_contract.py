@@ -61,5 +61,6 @@ def test_traffic_only_for_dispatched_kernels():
     ks = tj["c5_direct"]["kernels"]
     assert t5 == sum(v["hbm_bytes"] for k, v in ks.items()
                      if k.split("<")[0] in ("k_stream_trigger_p", "k_direct_mfma", "k_stream_update"))
+    assert "k_stream_trigger_p + k_direct_mfma" in src5
     # algorithmic bytes: traffic within a small factor (no silent re-reads on config 2)
     assert t2 < 1.1 * 4096 * (3 * 1024 * 2 + 4 * 3 + 8)
