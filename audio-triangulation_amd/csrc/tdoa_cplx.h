@@ -15,6 +15,10 @@
 
 namespace {
 
+__device__ __forceinline__ f2 v_xx(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ f2 v_yy(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ f2 v_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 #ifdef TDOA_ASM_MUL_S
 // products by compile-time twiddles in an SGPR pair as pinned asm pairs
 // (tdoa_phat_r16.hip, whose scheduling measured better with them)
@@ -37,9 +41,6 @@ TDOA_PK_MUL_S(c_negmulconj_s, " neg_lo:[0,1] neg_hi:[0,1]", " neg_lo:[0,1,0] neg
 // products by compile-time twiddles (SGPR-pair constants) as plain packed-vector
 // code: splats become op_sel, so each is still v_pk_mul + v_pk_fma, but the
 // post-RA scheduler sees them and fills the packed-result hazard slots
-__device__ __forceinline__ f2 v_xx(f2 a) { return __builtin_shufflevector(a, a, 0, 0); }
-__device__ __forceinline__ f2 v_yy(f2 a) { return __builtin_shufflevector(a, a, 1, 1); }
-__device__ __forceinline__ f2 v_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 c_mul_s(f2 a, f2 w) { return v_fma(v_yy(a), f2{-w.y, w.x}, v_xx(a) * w); }
 __device__ __forceinline__ f2 c_mulconj_s(f2 a, f2 w) { return v_fma(v_yy(a), f2{w.y, w.x}, v_xx(a) * f2{w.x, -w.y}); }
 __device__ __forceinline__ f2 c_negmul_s(f2 a, f2 w) { return c_mul_s(a, f2{-w.x, -w.y}); }
@@ -113,18 +114,27 @@ __device__ __forceinline__ f2 c_i(f2 x)
 
 // x / sqrt(|x|^2 + e2): |x|^2 + e2 as two fma (no clamp instruction; a zero
 // bin stays 0, and for every other bin of an integer frame e2 is far below the
-// fp32 resolution of |x|^2), rsq, scale.  The rsq lands in the low dword of a
-// pair whose high dword op_sel_hi ignores (no copy to build {r, r}).  The
-// multiply opens with s_nop 0: a transcendental result read by the next VALU
-// needs one wait state, and the compiler does not pad ahead of asm
+// fp32 resolution of |x|^2), rsq, scale.  Plain vector code: the splat {r, r}
+// folds into op_sel_hi (no copy), and the compiler sees the rsq result's
+// wait state (the pinned-asm form carried an unconditional s_nop 0)
 __device__ __forceinline__ f2 c_unit(f2 x, float e2)
 {
+#ifdef TDOA_ASM_MUL_S
+    // k_frame16 (tdoa_phat_r16.hip) keeps the pinned form, which measured
+    // faster there (4.09 vs 4.10 ms per config-3 step, 110.0 vs 112.3 ms per
+    // config-4 step, together with its DIF twiddles); the asm multiply opens
+    // with s_nop 0 because the compiler does not pad a transcendental result
+    // ahead of inline asm
     const float m = __builtin_fmaf(x.x, x.x, __builtin_fmaf(x.y, x.y, e2));
     f2 rr;
     rr.x = __builtin_amdgcn_rsqf(m);
     f2 y;
     asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(rr));
     return y;
+#else
+    const float r = __builtin_amdgcn_rsqf(__builtin_fmaf(x.x, x.x, __builtin_fmaf(x.y, x.y, e2)));
+    return x * f2{r, r};
+#endif
 }
 
 // W_32^k = e^{-2 pi i k / 32}, k = 1..7 (the others by symmetry)
@@ -159,6 +169,84 @@ __device__ __forceinline__ f2 tw_only(f2 x, int k)
     if (k < 8)
         return INV ? c_mulconj_s(x, w32c(k)) : c_mul_s(x, w32c(k));
     return INV ? c_negmul_s(x, w32c(16 - k)) : c_negmulconj_s(x, w32c(16 - k));
+}
+
+// cos / sin (2 pi q / 32), q = 0..16, in double: the FMA butterfly constants
+// below are rounded once from their exact quotients
+__device__ constexpr double COS32D[17] = {
+    1.0, 0.98078528040323043, 0.92387953251128674, 0.83146961230254524, 0.70710678118654752,
+    0.55557023301960218, 0.38268343236508977, 0.19509032201612826, 0.0, -0.19509032201612826,
+    -0.38268343236508977, -0.55557023301960218, -0.70710678118654752, -0.83146961230254524,
+    -0.92387953251128674, -0.98078528040323043, -1.0};
+__device__ __forceinline__ f2 v_sw(f2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+
+// DIT butterfly (a, b) <- (a + W b, a - W b), W = W_32^{+-q} (q compile-time
+// after unrolling), in three packed FMAs for a non-trivial W (Goedecker's
+// tangent form; the swaps fold into op_sel):
+//   |Re W| >= |Im W|: W b = c (b + i tau b), tau = Im W / Re W, c = Re W
+//       u = fma(swap(b), (-tau, tau), b);  a +- c u
+//   otherwise:       W b = i s (b - i kap b), kap = Re W / Im W, s = Im W
+//       u = fma(swap(b), (kap, -kap), b);  a +- i s u = fma(swap(u), (-+s, +-s), a)
+// W = 1 and W = -+i are one packed add each.
+template <bool INV>
+__device__ __forceinline__ void bfly_dit(f2 &a, f2 &b, int q)
+{
+    const f2 t = a;
+    if (q == 0) {
+        a = t + b;
+        b = t - b;
+        return;
+    }
+    if (q == 8) {  // W = -i (forward), +i (inverse)
+        a = INV ? c_add_i(t, b) : c_add_mi(t, b);
+        b = INV ? c_add_mi(t, b) : c_add_i(t, b);
+        return;
+    }
+    // sin(2 pi q / 32) = cos(2 pi (8 - q) / 32); forward Im W = -sin
+    const double wr = COS32D[q], si = COS32D[q < 8 ? 8 - q : q - 8];
+    const double im = INV ? si : -si;
+    if (__builtin_fabs(wr) >= __builtin_fabs(im)) {
+        const float tau = (float)(im / wr), c = (float)wr;
+        const f2 u = v_fma(v_sw(b), f2{-tau, tau}, b);
+        a = v_fma(u, f2{c, c}, t);
+        b = v_fma(u, f2{-c, -c}, t);
+    } else {
+        const float kap = (float)(wr / im), s = (float)im;
+        const f2 u = v_fma(v_sw(b), f2{kap, -kap}, b);
+        a = v_fma(v_sw(u), f2{-s, s}, t);
+        b = v_fma(v_sw(u), f2{s, -s}, t);
+    }
+}
+
+// Radix-2 DIT DFT-32 with FMA butterflies, natural order in and out (the
+// input bit reversal is register renaming).  HALF_ZERO: inputs 16..31 are
+// zero, so the first stage is a copy.  34 non-trivial butterflies at three
+// packed FMAs: 194 instructions (162 with HALF_ZERO) against the DIF form's
+// 228 (197).
+template <bool INV, bool HALF_ZERO>
+__device__ __forceinline__ void fft32d(f2 (&x)[32])
+{
+    f2 v[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++)
+        v[i] = x[brev5(i)];
+#pragma unroll
+    for (int g = 0; g < 32; g += 2) {
+        if (HALF_ZERO)
+            v[g + 1] = v[g];
+        else
+            bfly_dit<INV>(v[g], v[g + 1], 0);
+    }
+#pragma unroll
+    for (int m = 4; m <= 32; m *= 2)
+#pragma unroll
+        for (int g = 0; g < 32; g += m)
+#pragma unroll
+            for (int j = 0; j < m / 2; j++)
+                bfly_dit<INV>(v[g + j], v[g + j + m / 2], j * (32 / m));
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        x[k] = v[k];
 }
 
 // In-place radix-2 DIF DFT-32 on packed primitives: natural-order input, X[k]

@@ -195,7 +195,7 @@ struct Lane {
 template <bool INV, bool HALF_ZERO>
 __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *tile)
 {
-    fft32p<INV, HALF_ZERO>(v);
+    fft32d<INV, HALF_ZERO>(v);
     wave_lds_sync();  // after the previous pass's row reads of this tile
     const int wo = 8 * L.cs;
 #pragma unroll
@@ -207,7 +207,7 @@ __device__ __forceinline__ void fft_col_lds(const Lane &L, f2 (&v)[32], char *ti
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int k = k0 + i;
-            f2 x = v[brev5(k)];
+            f2 x = v[k];
             if (k)
                 x = INV ? c_mulconj(x, tw[i]) : c_mul(x, tw[i]);
             sts_f2(tile, wo + P1K_ROW * slot(k), x);
@@ -223,10 +223,10 @@ __device__ __forceinline__ void fft_row_fwd(const Lane &L, const char *tile, f2 
 #pragma unroll
     for (int n = 0; n < 32; n++)
         v[n] = lds_f2(tile, ro + 8 * slot(n));
-    fft32p<false, false>(v);
+    fft32d<false, false>(v);
 #pragma unroll
     for (int k = 0; k < 32; k++)
-        V[k] = v[brev5(k)];
+        V[k] = v[k];
 }
 }  // namespace
 
@@ -328,31 +328,44 @@ __device__ __forceinline__ void lean_forward_cross(const Lane &L, const uint32_t
     }
 }
 
+// acc + d W_32^k (forward W), k compile-time after unrolling: two chained
+// packed FMAs (one packed add for W = 1, -i)
+__device__ __forceinline__ f2 cmac_fwd(f2 acc, f2 d, int k)
+{
+    if (k == 0)
+        return acc + d;
+    if (k == 8)
+        return c_add_mi(acc, d);
+    const f2 w = f2{(float)COS32D[k], -(float)COS32D[k < 8 ? 8 - k : k - 8]};
+    return v_fma(v_yy(d), f2{-w.y, w.x}, v_fma(v_xx(d), w, acc));
+}
+
 // second half of the pruned inverse (fft_row_inv) in two groups of 8 residue
-// pairs, so at most half a row of tile values is in registers at a time
+// pairs, so at most half a row of tile values is in registers at a time:
+// y0 = sum of the row, y31 = sum_i (v_i - v_{i+16}) W_32^i accumulated by
+// FMA in two chains per group
 __device__ __forceinline__ void lean_row_inv(const Lane &L, const char *tile, f2 &y0, f2 &y31)
 {
     const int ro = P1K_ROW * L.cs;
     f2 ga[2], gd[2];
 #pragma unroll
     for (int g = 0; g < 2; g++) {
-        f2 a[8], d[8];
+        f2 a[8], c[2];
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const f2 v = lds_f2(tile, ro + 8 * slot(8 * g + i));
             const f2 u = lds_f2(tile, ro + 8 * slot(8 * g + i + 16));
             a[i] = v + u;
-            d[i] = tw_only<false>(v - u, 8 * g + i);
+            const f2 d = v - u;
+            c[i & 1] = i < 2 ? tw_only<false>(d, 8 * g + i) : cmac_fwd(c[i & 1], d, 8 * g + i);
         }
 #pragma unroll
         for (int h = 4; h >= 1; h >>= 1)
 #pragma unroll
-            for (int r = 0; r < h; r++) {
+            for (int r = 0; r < h; r++)
                 a[r] = a[r] + a[r + h];
-                d[r] = d[r] + d[r + h];
-            }
         ga[g] = a[0];
-        gd[g] = d[0];
+        gd[g] = c[0] + c[1];
         pin(ga[g]);
         pin(gd[g]);
     }
@@ -626,8 +639,11 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             for (int c = 0; c < 4; c++)
                 if (ok[c])
                     wsc[(p * P1K_KPAD + ck[c]) * 2 + hw] = wv[p][c];
-        if (L.lane < 3)  // lag slot 127 of every pair: the padding tuple
-            wsc[(L.lane * P1K_KPAD + P1K_KPAD - 1) * 2 + hw] = -INFINITY;
+        {
+            const int ft = fresh_tid();  // (lane, half-wave) not held across the phases
+            if ((ft & 31) < 3)  // lag slot 127 of every pair: the padding tuple
+                wsc[((ft & 31) * P1K_KPAD + P1K_KPAD - 1) * 2 + ((ft >> 5) & 1)] = -INFINITY;
+        }
         wave_lds_sync();  // the gathers read other lanes' score slots
         LEAN_MARK();
         float gv[2] = {-INFINITY, -INFINITY};
