@@ -20,6 +20,19 @@
 
 namespace {
 
+// 16-B chunk k (8 int16 samples) of row `row` of a frame batch: int16 rows, or
+// the streaming batch's 8-bit rows (kp.frames_u8) widened from 8 bytes
+__device__ __forceinline__ uint4 frame_chunk(const tdoa_kparams &kp, const int16_t *frames, int64_t row, int k)
+{
+    if (kp.frames_u8) {
+        const uint2 b = reinterpret_cast<const uint2 *>(reinterpret_cast<const uint8_t *>(frames) +
+                                                        row * kp.N)[k];
+        return make_uint4(__builtin_amdgcn_perm(0u, b.x, 0x0C010C00u), __builtin_amdgcn_perm(0u, b.x, 0x0C030C02u),
+                          __builtin_amdgcn_perm(0u, b.y, 0x0C010C00u), __builtin_amdgcn_perm(0u, b.y, 0x0C030C02u));
+    }
+    return reinterpret_cast<const uint4 *>(frames + row * kp.N)[k];
+}
+
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 
@@ -138,8 +151,9 @@ __device__ void stage_frames(const tdoa_kparams &kp, const Smem &sm, const int16
             const int k = c - r * cpr;
             if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
                 const int fl = r / kp.M, m = r - fl * kp.M;
-                v = reinterpret_cast<const uint4 *>(
-                    frames + ((int64_t)kp.frame_ids[f0 + fl] * kp.M + m) * kp.N)[k];
+                v = frame_chunk(kp, frames, (int64_t)kp.frame_ids[f0 + fl] * kp.M + m, k);
+            } else if (kp.frames_u8) {
+                v = frame_chunk(kp, frames, f0 * kp.M + r, k);
             } else {
                 v = src[c];
             }

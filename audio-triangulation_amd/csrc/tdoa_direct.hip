@@ -380,7 +380,9 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
             const int r = c / cpr, k = c - r * cpr;
             if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
                 const int fl = r / kp.M, m = r - fl * kp.M;
-                v[i] = reinterpret_cast<const uint4 *>(frames + ((int64_t)kp.frame_ids[f0 + fl] * kp.M + m) * kp.N)[k];
+                v[i] = frame_chunk(kp, frames, (int64_t)kp.frame_ids[f0 + fl] * kp.M + m, k);
+            } else if (kp.frames_u8) {
+                v[i] = frame_chunk(kp, frames, f0 * kp.M + r, k);
             } else {
                 v[i] = reinterpret_cast<const uint4 *>(frames + f0 * kp.M * kp.N)[c];
             }

@@ -105,6 +105,10 @@ struct tdoa_kparams {
     // (the persistent trigger writes each frame at its stream's index); null:
     // frame f is frames[f]
     const int32_t *frame_ids;
+    // the streaming batch's frames are 8-bit ADC samples ([.][M][N] bytes, the
+    // capture ring's values: half the bytes of int16 copies), widened to int16
+    // when staged
+    int32_t frames_u8;
     // least-squares refinement (tdoa_ls.hip)
     const float *mic_xy;       // [M][2] metres
     float fs, c, height;
@@ -136,6 +140,8 @@ struct tdoa_stream_params {
     int64_t *pos;             // [1] samples consumed (device clock)
     int64_t *ring_start;      // [S] sample index of the last trigger (rings restart there)
     int32_t *count;           // [1] frames triggered this step
+    int32_t *count_next;      // [1] the next step's counter: zeroed by this step's trigger
+                              // (two counters alternate by hop parity: no memset node)
     int32_t *ids;             // [S] compact slot -> stream
     int64_t *end;             // [S] samples consumed at the trigger
     int16_t *frames;          // [S][M][N] triggered frames, compact

@@ -1,8 +1,11 @@
 // tdoa_stream.cpp -- host side of the streaming pipeline (include/tdoa.h,
 // kernels in tdoa_stream.hip): device state, the per-hop kernel sequence
-//   memset(count) -> k_stream_trigger -> k_direct_mfma (device-sized batch,
-//   EMA + grid on the EMA scores fused) -- or, for shapes that kernel does not
-//   solve, k_direct -> k_stream_update -- and its hipGraph capture / replay.
+//   k_stream_trigger -> k_direct_mfma (device-sized batch, EMA + grid on the
+//   EMA scores fused) -- or, for shapes that kernel does not solve, k_direct ->
+//   k_stream_update -- and its hipGraph capture / replay.  The hop's trigger
+//   counter alternates between two slots by hop parity: the trigger zeroes the
+//   other slot for the next hop (a memset node cost 3.9 us per hop), so the
+//   two parities are two captured graphs.
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -27,11 +30,12 @@ struct tdoa_stream {
     void *mem = nullptr;  // one allocation for all state
     size_t mem_bytes = 0;
     int use_graph;
-    // captured step graph and what it was captured for
-    hipGraphExec_t exec = nullptr;
-    hipGraph_t graph = nullptr;
-    tdoa_stream_outputs g_out{};
-    hipStream_t g_stream = nullptr;
+    int64_t hop = 0;  // steps enqueued since create / reset: the counter slot's parity
+    // captured step graphs (one per counter parity) and what they were captured for
+    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    hipGraph_t graph[2] = {nullptr, nullptr};
+    tdoa_stream_outputs g_out[2]{};
+    hipStream_t g_stream[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -70,17 +74,19 @@ tdoa_stream_kout to_kout(const tdoa_stream_outputs *o)
     return k;
 }
 
-// the per-hop kernel sequence
-int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
+// the per-hop kernel sequence; par: the hop's counter slot
+int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s, int par)
 {
-    const tdoa_stream_params &sp = st->sp;
-    S_TRY(hipMemsetAsync(sp.count, 0, sizeof(int32_t), s));
+    tdoa_stream_params sp = st->sp;
+    sp.count = st->sp.count + par;
+    sp.count_next = st->sp.count + (1 - par);
     bool by_id = false;  // where the trigger put the frames: the layout DIRECT reads
     int rc = tdoa_launch_stream_trigger(sp, st->S, s, &by_id);
     if (rc)
         return rc;
     tdoa_kparams kp = st->kp;
     kp.frame_ids = by_id ? sp.ids : nullptr;
+    kp.frames_u8 = 1;  // the triggers write 8-bit frames
     if (tdoa_direct_ema_fits(kp)) {
         // k_direct_mfma runs the EMA and the grid on the EMA scores itself:
         // results straight into the caller's slots, no fresh-score round trip
@@ -105,14 +111,14 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s)
     return tdoa_launch_stream_update(sp, st->kp, to_kout(out), st->S, s);
 }
 
-void drop_graph(tdoa_stream *st)
+void drop_graph(tdoa_stream *st, int par)
 {
-    if (st->exec)
-        (void)hipGraphExecDestroy(st->exec);
-    if (st->graph)
-        (void)hipGraphDestroy(st->graph);
-    st->exec = nullptr;
-    st->graph = nullptr;
+    if (st->exec[par])
+        (void)hipGraphExecDestroy(st->exec[par]);
+    if (st->graph[par])
+        (void)hipGraphDestroy(st->graph[par]);
+    st->exec[par] = nullptr;
+    st->graph[par] = nullptr;
 }
 
 }  // namespace
@@ -154,8 +160,8 @@ extern "C" int tdoa_stream_create(tdoa_ctx *ctx, int32_t num_streams, int32_t ho
         off = (off + bytes + 255) & ~(size_t)255;
         return o;
     };
-    const size_t o_pos = take(8), o_count = take(4), o_rs = take(S * 8), o_ids = take(S * 4),
-                 o_end = take(S * 8), o_frames = take(S * M * N * 2), o_fresh = take(S * P * K * 8),
+    const size_t o_pos = take(8), o_count = take(8), o_rs = take(S * 8), o_ids = take(S * 4),
+                 o_end = take(S * 8), o_frames = take(S * M * N), o_fresh = take(S * P * K * 8),
                  o_fl = take(S * P * 4), o_fg = take(S), o_est = take(S * P * K * 8),
                  o_last = take(S * 8), o_stats = take(16);
     if (hipMalloc(&st->mem, off) != hipSuccess) {
@@ -199,13 +205,18 @@ extern "C" int tdoa_stream_step(tdoa_stream *st, const tdoa_stream_outputs *out,
         return sfail(TDOA_ERR_INVALID, "tdoa_stream_step: NULL stream");
     S_TRY(hipSetDevice(st->device));
     hipStream_t s = (hipStream_t)stream;
-    if (!st->use_graph || !s)
-        return enqueue_step(st, out, s);
+    const int par = (int)(st->hop & 1);
+    if (!st->use_graph || !s) {
+        const int rc = enqueue_step(st, out, s, par);
+        if (!rc)
+            st->hop++;
+        return rc;
+    }
     const tdoa_stream_outputs want = out ? *out : tdoa_stream_outputs{};
-    if (!st->exec || st->g_stream != s || std::memcmp(&want, &st->g_out, sizeof want) != 0) {
-        drop_graph(st);
+    if (!st->exec[par] || st->g_stream[par] != s || std::memcmp(&want, &st->g_out[par], sizeof want) != 0) {
+        drop_graph(st, par);
         S_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_step(st, out, s);
+        const int rc = enqueue_step(st, out, s, par);
         hipGraph_t g = nullptr;
         const hipError_t ec = hipStreamEndCapture(s, &g);
         if (rc) {
@@ -215,12 +226,13 @@ extern "C" int tdoa_stream_step(tdoa_stream *st, const tdoa_stream_outputs *out,
         }
         if (ec != hipSuccess)
             return sfail(TDOA_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
-        st->graph = g;
-        S_TRY(hipGraphInstantiate(&st->exec, g, nullptr, nullptr, 0));
-        st->g_out = want;
-        st->g_stream = s;
+        st->graph[par] = g;
+        S_TRY(hipGraphInstantiate(&st->exec[par], g, nullptr, nullptr, 0));
+        st->g_out[par] = want;
+        st->g_stream[par] = s;
     }
-    S_TRY(hipGraphLaunch(st->exec, s));
+    S_TRY(hipGraphLaunch(st->exec[par], s));
+    st->hop++;
     return TDOA_OK;
 }
 
@@ -230,6 +242,7 @@ extern "C" int tdoa_stream_reset(tdoa_stream *st, void *stream)
         return sfail(TDOA_ERR_INVALID, "tdoa_stream_reset: NULL stream");
     S_TRY(hipSetDevice(st->device));
     S_TRY(hipMemsetAsync(st->mem, 0, st->mem_bytes, (hipStream_t)stream));
+    st->hop = 0;  // both counter slots are zero again
     return TDOA_OK;
 }
 
@@ -259,7 +272,8 @@ extern "C" int tdoa_stream_destroy(tdoa_stream *st)
         return TDOA_OK;
     (void)hipSetDevice(st->device);
     (void)hipDeviceSynchronize();
-    drop_graph(st);
+    drop_graph(st, 0);
+    drop_graph(st, 1);
     (void)hipFree(st->mem);
     delete st;
     return TDOA_OK;

@@ -74,6 +74,8 @@ __device__ __forceinline__ void block_exclusive_scan(int &v1, long long &v2, int
 
 __global__ void __launch_bounds__(TPB) k_stream_trigger(tdoa_stream_params sp)
 {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && sp.count_next)
+        *sp.count_next = 0;  // the next hop's counter (last read by the previous hop)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int M = sp.M, N = sp.N, H = sp.H, L = N + H - 1, tid = threadIdx.x;
     int16_t *xs = (int16_t *)smem;                                   // [M][L]
@@ -181,10 +183,14 @@ __global__ void __launch_bounds__(TPB) k_stream_trigger(tdoa_stream_params sp)
         sp.ring_start[s] = end;
     }
     __syncthreads();
-    int16_t *dst = sp.frames + (size_t)slot * M * N;
-    for (int i = tid; i < M * N; i += TPB) {
-        const int m = i / N, n = i - m * N;
-        dst[i] = xs[m * L + a + n];
+    // the frame as 8-bit samples (the capture's values; DIRECT widens them,
+    // kp.frames_u8), four per dword store
+    uint32_t *dst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(sp.frames) + (size_t)slot * M * N);
+    for (int i = tid; i < M * N / 4; i += TPB) {
+        const int m = (4 * i) / N, n = 4 * i - m * N;
+        const int16_t *x = xs + m * L + a + n;
+        dst[i] = (uint32_t)(uint8_t)x[0] | (uint32_t)(uint8_t)x[1] << 8 | (uint32_t)(uint8_t)x[2] << 16 |
+                 (uint32_t)(uint8_t)x[3] << 24;
     }
 }
 
@@ -224,6 +230,8 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
     extern __shared__ __attribute__((aligned(16))) uint32_t stage_all[];  // [NWB waves][3 H M / 4]
     __shared__ int nfired[NWB], slot_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && sp.count_next)
+        *sp.count_next = 0;  // the next hop's counter (last read by the previous hop)
     uint32_t *stage = stage_all + wv * (3 * H * M / 4);
     const int64_t GW = (int64_t)gridDim.x * NWB;
     const int64_t s0 = (int64_t)blockIdx.x * NWB;  // the workgroup's first stream of an iteration
@@ -424,13 +432,18 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
             // at the stream's own index: the compact list (ids, end) is
             // written once per workgroup at the end (thousands of same-address
             // slot atomics per hop serialise in L2: 53.5 vs 36.4 us)
-            int16_t *dst = sp.frames + (size_t)s * M * N;
-#pragma unroll 4
-            for (int t = 0; t < N / 64; t++) {
-                const int n = lane + 64 * t;
+            // as 8-bit samples (DIRECT widens them, kp.frames_u8): four per
+            // dword store, half the bytes of int16 copies
+            uint32_t *dst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(sp.frames) + (size_t)s * M * N);
+#pragma unroll 2
+            for (int t = 0; t < N / 256; t++) {
+                const int n = 4 * (lane + 64 * t);
 #pragma unroll
-                for (int m = 0; m < M; m++)
-                    dst[(size_t)m * N + n] = (int16_t)sb[(a + n) * M + m];
+                for (int m = 0; m < M; m++) {
+                    const uint8_t *q = sb + (a + n) * M + m;
+                    dst[((size_t)m * N + n) / 4] = (uint32_t)q[0] | (uint32_t)q[M] << 8 | (uint32_t)q[2 * M] << 16 |
+                                                   (uint32_t)q[3 * M] << 24;
+                }
             }
         }
         rs = rsn;
