@@ -125,7 +125,8 @@ __device__ __forceinline__ void wave_best(T &v, int &i)
 }
 
 // One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
-// by this wave before the call); M8: a [128] LDS scratch row of this wave;
+// by this wave before the call); M8: [4][128] LDS scratch rows of this wave
+// (16-B aligned);
 // tiles / rng: the entry table (LDS or global).  Returns the max L (best) and
 // its tuple index in first-cell order (bu, INT_MAX when no L exceeded the
 // lowest value).  Every lane returns the same pair.
@@ -143,7 +144,8 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
 #pragma unroll
     for (int j = 0; j < JT; j++)
         bt[j] = (lane + 64 * j < NT) ? (T)0 : low;
-    if (P <= 8) {  // few pairs: a direct range loop
+    if (P <= 8) {  // few pairs: a direct range loop (the grouped maxima below
+        // measured slower at config 3: 4.21 vs 4.09 ms per step)
 #pragma unroll
         for (int j = 0; j < JT; j++) {
             const int t = lane + 64 * j;
@@ -161,32 +163,56 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             }
         }
     } else {
-        // many pairs: per pair the 8-wide running maxima M8[k] = max w[k..k+7]
-        // (clamped to K - 1); a range of width <= 16 is max(M8[lo],
-        // M8[max(lo, hi - 7)]) -- independent reads, not a dependent chain.
-        // (Four pairs' rows per sync measured no faster: the pass is bound
-        // by LDS issue, not by its round trips.)
-        for (int p = 0; p < P; p++) {
-            const T *w = Wl + p * K;
-            wave_lds_sync();  // previous pair's M8 reads come first
-            for (int k = lane; k < K; k += 64) {
-                T m = w[k];
+        // per group of four pairs, the 8-wide running maxima M8[g][k] = max
+        // w[k..min(k + 7, K - 1)]: lane 16 g + q builds k = 8q .. 8q + 7 of pair
+        // p0 + g from 15 reads (suffix / prefix maxima, two 16-B stores); then a
+        // range of width <= 16 is max(M8[lo], M8[max(lo, hi - 7)]) -- two reads
+        // per entry and pair, and two wave syncs per four pairs (one pair per
+        // sync, eight reads per element, bound the pass on LDS issue before:
+        // config 4 109.7 -> 108.3 ms per step)
+        const int gq = lane >> 4, q8 = 8 * (lane & 15);
+        for (int p0 = 0; p0 < P; p0 += 4) {
+            wave_lds_sync();  // the previous group's M8 reads come first
+            if (p0 + gq < P && q8 < K) {
+                const T *w = Wl + (p0 + gq) * K;
+                T x[15];
+#pragma unroll
+                for (int d = 0; d < 15; d++)
+                    x[d] = w[q8 + d < K ? q8 + d : K - 1];
+#pragma unroll
+                for (int d = 6; d >= 0; d--)  // suffix maxima of x[0..7]
+                    x[d] = vmax<T>(x[d], x[d + 1]);
+#pragma unroll
+                for (int d = 9; d < 15; d++)  // prefix maxima of x[8..14]
+                    x[d] = vmax<T>(x[d], x[d - 1]);
+                T o[8];
+                o[0] = x[0];
 #pragma unroll
                 for (int d = 1; d < 8; d++)
-                    m = vmax<T>(m, w[k + d < K ? k + d : K - 1]);
-                M8[k] = m;
+                    o[d] = vmax<T>(x[d], x[7 + d]);
+                T *dst = M8 + gq * 128 + q8;
+#pragma unroll
+                for (int d = 0; d < 8; d++)
+                    dst[d] = o[d];
             }
             wave_lds_sync();
 #pragma unroll
             for (int j = 0; j < JT; j++) {
                 const int t = lane + 64 * j;
                 if (t < NT) {
-                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                    T m = M8[lo];
-                    for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
-                        m = vmax<T>(m, M8[k]);
-                    m = vmax<T>(m, M8[hi - 7 > lo ? hi - 7 : lo]);
-                    bt[j] += m;
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const int p = p0 + g;
+                        if (p < P) {  // bounds summed in L's own pair order
+                            const T *m8 = M8 + g * 128;
+                            const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
+                            T m = m8[lo];
+                            for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
+                                m = vmax<T>(m, m8[k]);
+                            m = vmax<T>(m, m8[hi - 7 > lo ? hi - 7 : lo]);
+                            bt[j] += m;
+                        }
+                    }
                 }
             }
         }

@@ -171,6 +171,36 @@ def test_ema_streams_vs_oracle(oracle):
         last = now
 
 
+def test_ema_solve_many_pairs_branch_and_bound(oracle):
+    """tdoa_average_batch's grid solve at the config-4 geometry (8 mics, 28
+    pairs): the int64 k_grid_bb with the grouped running maxima of the bound
+    pass (P > 8), against the oracle's exhaustive scan, bit for bit -- random
+    EMA scores (weak bounds) and one stream of all-equal scores (ties)."""
+    loc = Localizer(num_mics=8, frame_len=2048, mic_xy=synth.circle_mics(8, 0.15))
+    P, K = loc.dims.P, loc.dims.K
+    lut = loc.lut().reshape(P, 101, 101)
+    Sn, steps = 12, 4
+    rng = np.random.default_rng(28)
+    est = torch.zeros((Sn, P, K), dtype=torch.int64, device="cuda")
+    best = torch.zeros((Sn, P), dtype=torch.int32, device="cuda")
+    est_ref = np.zeros((Sn, P, K), np.int64)
+    for t in range(steps):
+        fresh = rng.integers(-(1 << 40), 1 << 40, (Sn, P, K)).astype(np.int64)
+        fresh[0] = 12345  # every tuple ties: the first cell
+        dec = rng.uniform(0.05, 1.0, Sn).astype(np.float32)
+        solve = {"cell": torch.empty(Sn, dtype=torch.int32, device="cuda"),
+                 "max_L": torch.empty(Sn, dtype=torch.int64, device="cuda"),
+                 "xy": torch.empty((Sn, 2), dtype=torch.float32, device="cuda")}
+        loc.average(est, torch.from_numpy(fresh).cuda(), torch.from_numpy(dec).cuda(), best, solve)
+        for s in range(Sn):
+            for p in range(P):
+                est_ref[s, p], _ = oracle.average(est_ref[s, p], fresh[s, p], float(dec[s]))
+            mL, cell = oracle.grid_solve(est_ref[s], lut)
+            assert solve["cell"][s].item() == cell and solve["max_L"][s].item() == mL, (t, s)
+        assert (est.cpu().numpy() == est_ref).all()
+    loc.close()
+
+
 def test_reference_symbols_gpu_backed(oracle):
     """The reference-named per-frame entry points (tdoa_reference_abi.h)."""
     L = tdoa.load()
