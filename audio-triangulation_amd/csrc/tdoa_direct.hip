@@ -702,7 +702,8 @@ __global__ void __launch_bounds__(256) k_ref_buffer(int op, int16_t *__restrict_
                                                     const int16_t *__restrict__ ring, int head,
                                                     int64_t *__restrict__ power,
                                                     const int16_t *__restrict__ window, int n,
-                                                    int log2n)
+                                                    int log2n, int16_t *__restrict__ s1,
+                                                    int16_t *__restrict__ s2)
 {
     __shared__ int tot;
     __shared__ unsigned long long pw;
@@ -725,6 +726,11 @@ __global__ void __launch_bounds__(256) k_ref_buffer(int op, int16_t *__restrict_
             const int16_t y = (int16_t)(uint16_t)((x - off16) & 0xFFFFu);
             buf[i] = y;
             p += (long long)y * y;
+            if (s1) {  // the next two ops of the frame path on this output (ops 1, 2 below)
+                const int16_t y1 = (int16_t)(uint16_t)(((uint32_t)(uint16_t)y << 8) & 0xFFFFu);
+                s1[i] = y1;
+                s2[i] = (int16_t)(uint16_t)((uint32_t)(((int32_t)y1 * (int32_t)window[i]) >> 15) & 0xFFFFu);
+            }
         }
         atomicAdd(&pw, (unsigned long long)p);
         __syncthreads();
@@ -935,13 +941,13 @@ int tdoa_launch_average(const tdoa_kparams &kp, int64_t S, int64_t *est, const i
 }
 
 int tdoa_launch_ref_buffer(int op, int16_t *buf, const int16_t *ring, int head, int64_t *power,
-                           const int16_t *window, int n, void *stream)
+                           const int16_t *window, int n, void *stream, int16_t *s1, int16_t *s2)
 {
     int log2n = 0;
     while ((1 << log2n) < n)
         log2n++;
     hipLaunchKernelGGL(k_ref_buffer, dim3(1), dim3(256), 0, (hipStream_t)stream, op, buf, ring,
-                       head, power, window, n, log2n);
+                       head, power, window, n, log2n, s1, s2);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return hip_fail(e, "k_ref_buffer launch");

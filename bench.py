@@ -417,8 +417,10 @@ def main_config1(args, dev, ri):
                        "calls_per_frame": 7, "parallelism": f"dp{world} (per-frame, no collective)"},
             "parity": res["parity"],
             "roofline": None,
-            "note": "latency-bound plumbing: seven synchronous GPU-backed calls per frame "
-                    "(the batched API is configs 2-5)",
+            "note": "latency-bound plumbing: seven synchronous GPU-backed calls per frame, three GPU "
+                    "round trips (each write_out's launch also computes the buffer's normalize and "
+                    "window, returned by those calls when their buffer holds exactly write_out's "
+                    "output); the batched API is configs 2-5",
             "cpu_baseline": cpu_baseline_config1(args, res) if not args.no_cpu else None,
         }
         print(json.dumps(line), flush=True)

@@ -221,6 +221,18 @@ def test_reference_symbols_gpu_backed(oracle):
             assert (np.frombuffer(bytes(b.buffer), np.int16) == g["normalized"][k]).all()
             L.buffer_window(C.byref(b))
             assert (np.frombuffer(bytes(b.buffer), np.int16) == g["windowed"][k]).all()
+            # the fused write_out records its normalised / windowed output; a
+            # buffer changed after write_out must take its own launch
+            b2 = _lib.Buffer()
+            L.rolling_buffer_write_out(C.byref(rb), C.byref(b2))
+            x = np.frombuffer(bytes(b2.buffer), np.int16).copy()
+            x[k % 1024] ^= 0x35
+            C.memmove(b2.buffer, x.ctypes.data, 2048)
+            L.buffer_normalize_range(C.byref(b2))
+            y = oracle.normalize(x)
+            assert (np.frombuffer(bytes(b2.buffer), np.int16) == y).all()
+            L.buffer_window(C.byref(b2))
+            assert (np.frombuffer(bytes(b2.buffer), np.int16) == oracle.window(y, win)).all()
             k += 1
     # correlations_init / correlations_average with a deterministic clock
     clock = {"t": 5_000_000}
