@@ -33,6 +33,34 @@ __device__ __forceinline__ uint4 frame_chunk(const tdoa_kparams &kp, const int16
     return reinterpret_cast<const uint4 *>(frames + row * kp.N)[k];
 }
 
+// the same chunk of mic m of streaming slot `slot`, straight from the capture
+// ring (kp.frame_ring; dma_sampler.c:17-23 round-robin bytes): samples
+// ring_at + 8k + i (wrapping at ring_len), zero before the stream's first
+// sample -- the bytes the trigger scanned (k_stream_trigger_p)
+__device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, int64_t slot, int m, int k)
+{
+    const int M = kp.M;
+    const int64_t cl = kp.ring_len;
+    const uint8_t *cap = kp.frame_ring + (size_t)kp.frame_ids[slot] * cl * M + m;
+    const int64_t t0 = kp.frame_end[slot] - kp.N + 8 * k;  // absolute index of sample 8k
+    int64_t j = kp.frame_ring_at[slot] + 8 * k;
+    if (j >= cl)
+        j -= cl;
+    uint32_t b[8];
+    if (t0 >= 0 && j + 8 <= cl) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            b[i] = cap[(j + i) * M];
+    } else {  // the ring's end or the stream's start: sample by sample
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int64_t ji = j + i >= cl ? j + i - cl : j + i;
+            b[i] = t0 + i < 0 ? 0u : (uint32_t)cap[ji * M];
+        }
+    }
+    return make_uint4(b[0] | b[1] << 16, b[2] | b[3] << 16, b[4] | b[5] << 16, b[6] | b[7] << 16);
+}
+
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 
@@ -149,9 +177,9 @@ __device__ void stage_frames(const tdoa_kparams &kp, const Smem &sm, const int16
         if (ok) {
             r = c / cpr;
             const int k = c - r * cpr;
-            if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
+            if (kp.frame_ring) {  // streaming batch: frame f0 + r / M from its stream's ring
                 const int fl = r / kp.M, m = r - fl * kp.M;
-                v = frame_chunk(kp, frames, (int64_t)kp.frame_ids[f0 + fl] * kp.M + m, k);
+                v = ring_chunk(kp, f0 + fl, m, k);
             } else if (kp.frames_u8) {
                 v = frame_chunk(kp, frames, f0 * kp.M + r, k);
             } else {

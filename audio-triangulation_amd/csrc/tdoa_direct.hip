@@ -168,13 +168,16 @@ __device__ void argmax_prior_mf(const tdoa_kparams &kp, int64_t *scores, int *be
 // single-word tuples: the thread's <= GR tuple words and first cells were
 // loaded at the kernel's start (q, cl); per frame the key maximum over the
 // thread's tuples, the wave (DPP) and the workgroup (LDS, one barrier)
-template <int GR>
+// PC: the pair count at compile time (0: kp.P at run time) -- a fixed count
+// unrolls the pair loop, so a tuple's 2 P reads issue back to back instead of
+// one LDS round trip per pair (config 2 / 5: P = 3)
+template <int GR, int PC>
 __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t *red, const uint32_t (&q)[GR],
                         const int32_t (&cl)[GR], const tdoa_kout &out, int64_t f0, int nf,
                         uint32_t omask = 0xFFFFFFFFu)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6, nt = blockDim.x;
-    const int K = kp.K, P = kp.P, U = kp.U;
+    const int K = kp.K, P = PC ? PC : kp.P, U = kp.U;
     uint64_t best[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int r = 0; r < GR; r++) {
@@ -182,7 +185,10 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
             // frame-interleaved table: the slot's four frames in two 16-B reads
             typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
             i64x2 L01 = {0, 0}, L23 = {0, 0};
-            for (int p = 0; p < P; p++) {
+#pragma unroll
+            for (int p = 0; p < (PC ? PC : 4); p++) {  // single-word tuples: P <= 4
+                if (!PC && p >= P)
+                    break;
                 const i64x2 *sl = reinterpret_cast<const i64x2 *>(
                     scores + sidx<true>(0, p, (q[r] >> (8 * p)) & 0xFFu, P, K));
                 L01 += sl[0];
@@ -378,9 +384,9 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
         w[i] = make_uint4(0, 0, 0, 0);
         if (c < nchunk) {
             const int r = c / cpr, k = c - r * cpr;
-            if (kp.frame_ids) {  // streaming batch: frame f0 + r / M at its stream's index
+            if (kp.frame_ring) {  // streaming batch: frame f0 + r / M from its stream's ring
                 const int fl = r / kp.M, m = r - fl * kp.M;
-                v[i] = frame_chunk(kp, frames, (int64_t)kp.frame_ids[f0 + fl] * kp.M + m, k);
+                v[i] = ring_chunk(kp, f0 + fl, m, k);
             } else if (kp.frames_u8) {
                 v[i] = frame_chunk(kp, frames, f0 * kp.M + r, k);
             } else {
@@ -587,7 +593,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     // no [B][P][K] round trip through HBM and no second launch
     if (do_grid) {
         if constexpr (KEYGRID)
-            grid_mf<GR>(kp, sm.scores, reinterpret_cast<uint64_t *>(smem + tb.red), gq, gc, out, f0, nf, omask);
+        {
+            uint64_t *red = reinterpret_cast<uint64_t *>(smem + tb.red);
+            if (kp.P == 3)
+                grid_mf<GR, 3>(kp, sm.scores, red, gq, gc, out, f0, nf, omask);
+            else
+                grid_mf<GR, 0>(kp, sm.scores, red, gq, gc, out, f0, nf, omask);
+        }
         else
             grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf, nullptr, nullptr, omask);
     }

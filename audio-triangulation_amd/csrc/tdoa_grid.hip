@@ -170,11 +170,12 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
     int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
     uint16_t *rng = (uint16_t *)(smem + (size_t)NT * 8);                      // [NT][P]
-    // per wave: M8 [4][128] running maxima of four pairs (K <= 127), then the
-    // frame's scores Wl [P][K] (both 16-B aligned)
-    const size_t per_wave = ((size_t)(4 * 128 + PK) * sizeof(T) + 15) & ~(size_t)15;
+    // per wave: the solve's scratch M8 (tdoa_bb::bb_scratch), then the frame's
+    // scores Wl [P][K] (both 16-B aligned)
+    const int scr = tdoa_bb::bb_scratch(P, K);
+    const size_t per_wave = ((size_t)(scr + PK) * sizeof(T) + 15) & ~(size_t)15;
     T *M8 = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15) + (size_t)wave * per_wave);
-    T *Wl = M8 + 4 * 128;
+    T *Wl = M8 + scr;
     for (int e = tid; e < 2 * NT; e += blockDim.x)
         tiles[e] = kp.bb_tile[e];
     for (int e = tid; e < NT * P; e += blockDim.x)
@@ -258,7 +259,8 @@ int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, i
               hipStream_t st)
 {
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
-    const size_t per_wave = (((size_t)kp.P * kp.K + 4 * 128) * sizeof(T) + 15) & ~(size_t)15;
+    const size_t per_wave =
+        (((size_t)kp.P * kp.K + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 15) & ~(size_t)15;
     int nw = (int)((150 * 1024 - table) / per_wave);
     nw = nw > 16 ? 16 : nw;
     const size_t lds = table + (size_t)nw * per_wave;
@@ -292,7 +294,8 @@ bool bb_fits(const tdoa_kparams &kp)
     if (kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
         return false;
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
-    return kp.K <= 127 && table + ((size_t)kp.P * kp.K + 4 * 128) * sizeof(T) + 16 <= 150 * 1024;
+    return kp.K <= 127 &&
+           table + ((size_t)kp.P * kp.K + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 16 <= 150 * 1024;
 }
 
 int hip_fail(hipError_t e, const char *what)

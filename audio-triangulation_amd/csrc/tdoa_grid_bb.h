@@ -124,9 +124,17 @@ __device__ __forceinline__ void wave_best(T &v, int &i)
     i = __builtin_amdgcn_readlane(i, 63);
 }
 
+// LDS scratch elements per wave beside the frame's scores (a multiple of 4, so
+// the scores after it stay 16-B aligned): the sparse table's levels 2, 4, 8
+// [3][P K] for P <= 8, the grouped 8-wide maxima [4][128] otherwise
+__host__ __device__ constexpr int bb_scratch(int P, int K)
+{
+    return P <= 8 && 3 * P * K > 4 * 128 ? (3 * P * K + 3) & ~3 : 4 * 128;
+}
+
 // One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
-// by this wave before the call); M8: [4][128] LDS scratch rows of this wave
-// (16-B aligned);
+// by this wave before the call); M8: bb_scratch(P, K) LDS scratch elements of
+// this wave (16-B aligned);
 // tiles / rng: the entry table (LDS or global).  Returns the max L (best) and
 // its tuple index in first-cell order (bu, INT_MAX when no L exceeded the
 // lowest value).  Every lane returns the same pair.
@@ -144,21 +152,47 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
 #pragma unroll
     for (int j = 0; j < JT; j++)
         bt[j] = (lane + 64 * j < NT) ? (T)0 : low;
-    if (P <= 8) {  // few pairs: a direct range loop (the grouped maxima below
-        // measured slower at config 3: 4.21 vs 4.09 ms per step)
+    if (P <= 8) {
+        // few pairs: a sparse table of the frame's scores -- level j holds
+        // max w[i .. i + 2^j - 1] (j = 1, 2, 3 in M8) -- so the maximum over a
+        // range of width n is exactly max(Sj[lo], Sj[hi + 1 - 2^j]) with 2^j <= n
+        // < 2^(j+1) (n >= 16: plus level-3 windows between): two independent
+        // reads per entry and pair instead of n dependent ones (the range loop:
+        // 69 % of a config-3 wave).  A window that crosses into the next row
+        // is never read: both windows lie inside [lo, hi].
+        const int PK = P * K;
+        T *S2 = M8, *S4 = M8 + PK, *S8 = M8 + 2 * PK;
+        for (int i = lane; i < PK; i += 64)
+            S2[i] = vmax<T>(Wl[i], Wl[i + 1 < PK ? i + 1 : i]);
+        wave_lds_sync();
+        for (int i = lane; i < PK; i += 64)
+            S4[i] = vmax<T>(S2[i], S2[i + 2 < PK ? i + 2 : i]);
+        wave_lds_sync();
+        for (int i = lane; i < PK; i += 64)
+            S8[i] = vmax<T>(S4[i], S4[i + 4 < PK ? i + 4 : i]);
+        wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < JT; j++) {
             const int t = lane + 64 * j;
             if (t < NT) {
-                T b = 0;
-                for (int p = 0; p < P; p++) {
-                    const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                    const T *w = Wl + p * K;
-                    T m = w[lo];
-                    for (int k = lo + 1; k <= hi; k++)
-                        m = vmax<T>(m, w[k]);
-                    b += m;
+                T mp[8];
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p < P) {
+                        const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8, n = hi - lo + 1;
+                        const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
+                        const T *L = lv ? M8 + (lv - 1) * PK + p * K : Wl + p * K;
+                        T m = vmax<T>(L[lo], L[hi + 1 - (1 << lv)]);
+                        for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
+                            m = vmax<T>(m, L[k]);
+                        mp[p] = m;
+                    }
                 }
+                T b = 0;
+#pragma unroll
+                for (int p = 0; p < 8; p++)
+                    if (p < P)  // bounds summed in L's own pair order
+                        b += mp[p];
                 bt[j] = b;
             }
         }

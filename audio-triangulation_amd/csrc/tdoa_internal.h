@@ -101,10 +101,16 @@ struct tdoa_kparams {
     const uint16_t *bb_rng;    // [NT][P] lo | hi << 8
     const uint32_t *bb_tuples; // [U][TW] regrouped tuples
     const int32_t *bb_uidx;    // [U] their index in first-cell order
-    // DIRECT on the streaming batch: frame f of the batch is frames[frame_ids[f]]
-    // (the persistent trigger writes each frame at its stream's index); null:
-    // frame f is frames[f]
+    // DIRECT on the streaming batch read straight from the capture ring (the
+    // persistent trigger lists the firing streams and copies nothing): frame f
+    // of the batch is stream frame_ids[f]'s samples from ring index
+    // frame_ring_at[f] (absolute sample frame_end[f] - N; earlier than the
+    // stream's first sample reads as 0); frame_ring null: frame f is frames[f]
     const int32_t *frame_ids;
+    const uint8_t *frame_ring;     // [S][ring_len][M] 8-bit ADC bytes, round-robin
+    int64_t ring_len;
+    const int64_t *frame_end;      // [B] samples consumed at the trigger
+    const int64_t *frame_ring_at;  // [B] ring index of the frame's first sample
     // the streaming batch's frames are 8-bit ADC samples ([.][M][N] bytes, the
     // capture ring's values: half the bytes of int16 copies), widened to int16
     // when staged
@@ -144,7 +150,9 @@ struct tdoa_stream_params {
                               // (two counters alternate by hop parity: no memset node)
     int32_t *ids;             // [S] compact slot -> stream
     int64_t *end;             // [S] samples consumed at the trigger
-    int16_t *frames;          // [S][M][N] triggered frames, compact
+    int64_t *ring_at;         // [S] ring index of the slot's first frame sample
+                              // (persistent trigger: DIRECT reads the ring)
+    int16_t *frames;          // [S][M][N] triggered frames, compact (k_stream_trigger)
     int64_t *fresh;           // [S][P][K] their weighted scores (k_direct)
     int32_t *fresh_lags;      // [S][P]
     uint8_t *fresh_gate;      // [S]

@@ -80,13 +80,19 @@ int enqueue_step(tdoa_stream *st, const tdoa_stream_outputs *out, hipStream_t s,
     tdoa_stream_params sp = st->sp;
     sp.count = st->sp.count + par;
     sp.count_next = st->sp.count + (1 - par);
-    bool by_id = false;  // where the trigger put the frames: the layout DIRECT reads
+    bool by_id = false;  // where DIRECT finds the frames: the capture ring or compact copies
     int rc = tdoa_launch_stream_trigger(sp, st->S, s, &by_id);
     if (rc)
         return rc;
     tdoa_kparams kp = st->kp;
-    kp.frame_ids = by_id ? sp.ids : nullptr;
-    kp.frames_u8 = 1;  // the triggers write 8-bit frames
+    if (by_id) {  // listed only: DIRECT stages each frame from its stream's ring
+        kp.frame_ids = sp.ids;
+        kp.frame_ring = sp.capture;
+        kp.ring_len = sp.capture_len;
+        kp.frame_end = sp.end;
+        kp.frame_ring_at = sp.ring_at;
+    }
+    kp.frames_u8 = 1;  // k_stream_trigger's compact copies are 8-bit
     if (tdoa_direct_ema_fits(kp)) {
         // k_direct_mfma runs the EMA and the grid on the EMA scores itself:
         // results straight into the caller's slots, no fresh-score round trip
@@ -161,7 +167,7 @@ extern "C" int tdoa_stream_create(tdoa_ctx *ctx, int32_t num_streams, int32_t ho
         return o;
     };
     const size_t o_pos = take(8), o_count = take(8), o_rs = take(S * 8), o_ids = take(S * 4),
-                 o_end = take(S * 8), o_frames = take(S * M * N), o_fresh = take(S * P * K * 8),
+                 o_end = take(S * 8), o_at = take(S * 8), o_frames = take(S * M * N), o_fresh = take(S * P * K * 8),
                  o_fl = take(S * P * 4), o_fg = take(S), o_est = take(S * P * K * 8),
                  o_last = take(S * 8), o_stats = take(16);
     if (hipMalloc(&st->mem, off) != hipSuccess) {
@@ -183,6 +189,7 @@ extern "C" int tdoa_stream_create(tdoa_ctx *ctx, int32_t num_streams, int32_t ho
     sp.ring_start = (int64_t *)(b + o_rs);
     sp.ids = (int32_t *)(b + o_ids);
     sp.end = (int64_t *)(b + o_end);
+    sp.ring_at = (int64_t *)(b + o_at);
     sp.frames = (int16_t *)(b + o_frames);
     sp.fresh = (int64_t *)(b + o_fresh);
     sp.fresh_lags = (int32_t *)(b + o_fl);

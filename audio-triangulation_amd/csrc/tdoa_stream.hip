@@ -217,9 +217,10 @@ __device__ __forceinline__ int wave_scan_incl(int v)
 // Persistent: each wave walks streams gw, gw + GW, ... with the NEXT stream's
 // capture words and ring start already requested while it scans the current one
 // (a one-stream-per-wave form waited on its loads at the start of every wave:
-// 68 % of wave cycles in SQ_WAIT_ANY).  A firing stream's frame is written from
-// the words the wave already holds, staged through LDS (no second read of the
-// ring).
+// 68 % of wave cycles in SQ_WAIT_ANY).  A firing stream is only listed (stream,
+// end, ring index of the frame's first sample): DIRECT stages the frame from
+// the capture ring itself (kp.frame_ring), so no copy of it is written and
+// read back (10.7 MB per config-5 hop as 8-bit copies).
 constexpr int TRIG_NWB = 4;  // waves per workgroup: occupancy in steps of one wave per SIMD
 template <int G, int M>
 __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_params sp, int64_t S)
@@ -273,7 +274,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
     // this wave's triggered streams: lane i holds the i-th (stream, end)
     int my_n = 0;
     int my_id = 0;
-    int64_t my_end = 0;
+    int64_t my_end = 0, my_at = 0;
     if (s < S) {
         fetch(s, wc, shc);
         rs = sp.ring_start[s];
@@ -412,39 +413,16 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
             const int fl = __builtin_ctzll(fire);  // lowest lane = lowest candidates
             const int a = G * fl + __builtin_amdgcn_readlane(fi, fl);
             const int64_t end = pos + 1 + a;
+            // the frame is local samples a .. a + N - 1 (rolling_buffer.c:48-62
+            // order): DIRECT reads them from the ring (kp.frame_ring), no copy
             if (lane == my_n) {
                 my_id = (int)s;
                 my_end = end;
+                my_at = j0 + a >= cl ? j0 + a - cl : j0 + a;
             }
             ++my_n;
             if (lane == 0)
                 sp.ring_start[s] = end;
-            // the frame (local samples a .. a + N - 1 of every mic, rolling_buffer.c:48-62
-            // order) from the words in registers: rows 0..2 staged as [l][m] bytes
-            wave_lds_sync();  // the previous stream's stage reads come first
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-                for (int k = 0; k < CW; k++)
-                    stage[r * (H * M / 4) + lane * CW + k] = x[r][k];
-            wave_lds_sync();  // a wave's LDS operations complete in order
-            const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
-            // at the stream's own index: the compact list (ids, end) is
-            // written once per workgroup at the end (thousands of same-address
-            // slot atomics per hop serialise in L2: 53.5 vs 36.4 us)
-            // as 8-bit samples (DIRECT widens them, kp.frames_u8): four per
-            // dword store, half the bytes of int16 copies
-            uint32_t *dst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(sp.frames) + (size_t)s * M * N);
-#pragma unroll 2
-            for (int t = 0; t < N / 256; t++) {
-                const int n = 4 * (lane + 64 * t);
-#pragma unroll
-                for (int m = 0; m < M; m++) {
-                    const uint8_t *q = sb + (a + n) * M + m;
-                    dst[((size_t)m * N + n) / 4] = (uint32_t)q[0] | (uint32_t)q[M] << 8 | (uint32_t)q[2 * M] << 16 |
-                                                   (uint32_t)q[3 * M] << 24;
-                }
-            }
         }
         rs = rsn;
     }
@@ -465,6 +443,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
     if (lane < my_n) {
         sp.ids[o + lane] = my_id;
         sp.end[o + lane] = my_end;
+        sp.ring_at[o + lane] = my_at;
     }
 }
 
@@ -711,7 +690,7 @@ int tdoa_launch_stream_trigger(const tdoa_stream_params &sp, int64_t S, void *st
             launch_trigger_m<8>(sp, S, st);
         else
             launch_trigger_m<16>(sp, S, st);
-        *by_id = true;  // frames at their streams' indices, read through the id list
+        *by_id = true;  // firing streams listed only: DIRECT reads their frames from the ring
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : fail_hip(e, "k_stream_trigger_p launch");
     }
