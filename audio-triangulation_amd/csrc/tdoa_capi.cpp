@@ -218,7 +218,8 @@ struct tdoa_ctx {
     size_t cscratch_bytes = 0;
     void *d_tscratch = nullptr;  // [B][P][3] float peak scores (least squares)
     size_t tscratch_bytes = 0;
-    std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx
+    std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx | queries
+    int bb_wide = 0;              // a range wider than the queries encode: no k_grid_bb
     void *d_bb = nullptr;
     int bb_NT = 0;
     float *d_mic = nullptr;  // [M][2]
@@ -310,6 +311,28 @@ void build_lut(tdoa_ctx *c)
     build_bb_tiles(c);
 }
 
+// An entry's range [lo, hi] of pair p as k_grid_bb's sparse-table query
+// (tdoa_grid_bb.h): the LDS element offset o1 of the level-j window
+// max w[lo .. lo + 2^j - 1] (2^j <= n = hi - lo + 1 < 2^(j+1)) from the wave's
+// scores, and the distance d = n - 2^j of the second window, as o1 | d << 13;
+// ranges wider than 15 are marked wide (o1 = 0x1FFF: the kernel loops)
+uint16_t bb_query(int P, int K, int p, int lo, int hi)
+{
+    const int n = hi - lo + 1;
+    if (n > 15)
+        return 0x1FFF;  // wide: the table is not used (kp.bb_wide)
+    const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
+    const int PKp = (P * K + 3) & ~3, RW = K <= 96 ? 96 : 128;
+    int o1;
+    if (lv == 0)
+        o1 = p * K + lo;  // the scores themselves
+    else if (P <= 8)
+        o1 = lv * PKp + p * K + lo;  // levels [3][P][K] after the scores
+    else
+        o1 = PKp + (lv - 1) * 4 * RW + (p & 3) * RW + lo;  // [3][4][RW]: four pairs a group
+    return (uint16_t)(o1 | ((n - (1 << lv)) << 13));
+}
+
 // Tables of the exact branch-and-bound grid solve (k_grid_bb, tdoa_grid.hip):
 // the distinct tuples regrouped by the TILE x TILE block of grid cells their
 // first cell lies in (entries of at most 64 tuples, one per lane), and for
@@ -327,7 +350,7 @@ void build_bb_tiles(tdoa_ctx *c)
         members[(size_t)(y / TILE) * tx + x / TILE].push_back(u);
     }
     std::vector<int32_t> tile;
-    std::vector<uint16_t> rng;
+    std::vector<uint16_t> rng, qry;
     std::vector<uint32_t> tup;
     std::vector<int32_t> uidx;
     for (const auto &m : members)
@@ -347,11 +370,16 @@ void build_bb_tiles(tdoa_ctx *c)
                     hi[p] = std::max(hi[p], l);
                 }
             }
-            for (int p = 0; p < P; p++)
+            for (int p = 0; p < P; p++) {
                 rng.push_back((uint16_t)(lo[p] | (hi[p] << 8)));
+                qry.push_back(bb_query(P, c->K, p, lo[p], hi[p]));
+            }
         }
     const int NT = (int)tile.size() / 2;
     c->bb_NT = NT;
+    c->bb_wide = 0;
+    for (const uint16_t q : qry)
+        c->bb_wide |= (q & 0x1FFF) == 0x1FFF;
     auto put = [&](const void *src, size_t bytes) {
         const size_t at = c->bb_img.size();
         c->bb_img.resize(at + ((bytes + 15) & ~(size_t)15), 0);
@@ -363,6 +391,7 @@ void build_bb_tiles(tdoa_ctx *c)
     put(rng.data(), rng.size() * 2);
     put(tup.data(), tup.size() * 4);
     put(uidx.data(), uidx.size() * 4);
+    put(qry.data(), qry.size() * 2);
 }
 
 void free_device(tdoa_ctx *c)
@@ -658,6 +687,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
     kp.tuples = c->d_tuples;
     kp.tuple_cell = c->d_tuple_cell;
     kp.bb_NT = c->bb_NT;
+    kp.bb_wide = c->bb_wide;
     if (kp.bb_NT > 0) {
         if (hipMalloc(&c->d_bb, c->bb_img.size()) != hipSuccess ||
             hipMemcpy(c->d_bb, c->bb_img.data(), c->bb_img.size(), hipMemcpyHostToDevice) !=
@@ -674,6 +704,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         kp.bb_rng = (const uint16_t *)(b + a1);
         kp.bb_tuples = (const uint32_t *)(b + a2);
         kp.bb_uidx = (const int32_t *)(b + a3);
+        kp.bb_q = (const uint16_t *)(b + a3 + ((((size_t)c->U * 4) + 15) & ~(size_t)15));
     }
     *out = c;
     return TDOA_OK;

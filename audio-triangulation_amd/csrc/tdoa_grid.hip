@@ -169,17 +169,16 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
     const int P = kp.P, K = kp.K, NT = kp.bb_NT, PK = P * K;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
     int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
-    uint16_t *rng = (uint16_t *)(smem + (size_t)NT * 8);                      // [NT][P]
-    // per wave: the solve's scratch M8 (tdoa_bb::bb_scratch), then the frame's
-    // scores Wl [P][K] (both 16-B aligned)
-    const int scr = tdoa_bb::bb_scratch(P, K);
-    const size_t per_wave = ((size_t)(scr + PK) * sizeof(T) + 15) & ~(size_t)15;
-    T *M8 = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15) + (size_t)wave * per_wave);
-    T *Wl = M8 + scr;
+    uint16_t *qt = (uint16_t *)(smem + (size_t)NT * 8);                       // [NT][P]
+    // per wave: the frame's scores Wl [P][K], then the solve's sparse-table
+    // levels (tdoa_bb::bb_scratch), 16-B aligned
+    const size_t per_wave =
+        ((size_t)(tdoa_bb::bb_pk(P, K) + tdoa_bb::bb_scratch(P, K)) * sizeof(T) + 15) & ~(size_t)15;
+    T *Wl = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15) + (size_t)wave * per_wave);
     for (int e = tid; e < 2 * NT; e += blockDim.x)
         tiles[e] = kp.bb_tile[e];
     for (int e = tid; e < NT * P; e += blockDim.x)
-        rng[e] = kp.bb_rng[e];
+        qt[e] = kp.bb_q[e];
     __syncthreads();
 
     unsigned long long bbacc[8] = {};
@@ -191,7 +190,9 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
         {
             // the frame's P x K scores (10.4 KB at config 4): 16-B loads, eight per
             // lane in flight before their LDS stores (one element per load and
-            // iteration waited on every load in turn: ~40 HBM round trips a frame)
+            // iteration waited on every load in turn: ~40 HBM round trips a frame);
+            // nontemporal, so the streamed scores do not evict the entry tables'
+            // tuples from L2 (every evaluation reads them)
             const T *src = weighted + f * PK;
             const int nv = (int)(((size_t)PK * sizeof(T)) / 16);
             const bool vec = nv > 0 && (((uintptr_t)src | (uintptr_t)Wl) & 15) == 0;
@@ -204,7 +205,10 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 #pragma unroll
                     for (int i = 0; i < 8; i++) {  // clamped: unconditional loads
                         const int e = b + i * 64 + lane;
-                        t[i] = s4[e < nv ? e : nv - 1];
+                        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                        const v4u x = __builtin_nontemporal_load(
+                            reinterpret_cast<const v4u *>(&s4[e < nv ? e : nv - 1]));
+                        t[i] = make_uint4(x.x, x.y, x.z, x.w);
                     }
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -229,7 +233,7 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 #endif
         T best;
         int bu;
-        tdoa_bb::solve_wave<T, TWC, JT>(kp, Wl, M8, tiles, rng, lane, best, bu, bbacc);
+        tdoa_bb::solve_wave<T, TWC, JT>(kp, Wl, tiles, qt, lane, best, bu, bbacc);
         if (lane == 0) {
             const int ui = (bu < 0 || bu >= kp.U) ? 0 : bu;  // every L compared false: tuple 0
             const int cell = kp.tuple_cell[ui];
@@ -254,14 +258,16 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
 }
 
 
+constexpr size_t BB_LDS = 160 * 1024;  // k_grid_bb's LDS: the entry table + per-wave scratch and scores
+
 template <typename T, int TWC, int JT>
 int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
               hipStream_t st)
 {
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
     const size_t per_wave =
-        (((size_t)kp.P * kp.K + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 15) & ~(size_t)15;
-    int nw = (int)((150 * 1024 - table) / per_wave);
+        (((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 15) & ~(size_t)15;
+    int nw = (int)((BB_LDS - table) / per_wave);
     nw = nw > 16 ? 16 : nw;
     const size_t lds = table + (size_t)nw * per_wave;
     const void *kern = (const void *)k_grid_bb<T, TWC, JT>;
@@ -291,11 +297,11 @@ int launch_bb_jt(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted
 template <typename T>
 bool bb_fits(const tdoa_kparams &kp)
 {
-    if (kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile)
+    if (kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile || !kp.bb_q || kp.bb_wide)
         return false;
     const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
     return kp.K <= 127 &&
-           table + ((size_t)kp.P * kp.K + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 16 <= 150 * 1024;
+           table + ((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 16 <= BB_LDS;
 }
 
 int hip_fail(hipError_t e, const char *what)

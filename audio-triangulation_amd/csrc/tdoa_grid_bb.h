@@ -124,28 +124,47 @@ __device__ __forceinline__ void wave_best(T &v, int &i)
     i = __builtin_amdgcn_readlane(i, 63);
 }
 
-// LDS scratch elements per wave beside the frame's scores (a multiple of 4, so
-// the scores after it stay 16-B aligned): the sparse table's levels 2, 4, 8
-// [3][P K] for P <= 8, the grouped 8-wide maxima [4][128] otherwise
+// row stride of the grouped levels (P > 8): 8 lags per lane, 12 or 16 lanes
+__host__ __device__ constexpr int bb_row(int K) { return K <= 96 ? 96 : 128; }
+// the frame's scores per wave, padded to 16 B: the levels follow them
+__host__ __device__ constexpr int bb_pk(int P, int K) { return (P * K + 3) & ~3; }
+
+// LDS scratch elements per wave after the frame's scores: the sparse table's
+// levels 1, 2, 3 [3][P][K] (P <= 8, bb_pk apart), or the same levels of four
+// pairs at a time [3][4][row] otherwise
 __host__ __device__ constexpr int bb_scratch(int P, int K)
 {
-    return P <= 8 && 3 * P * K > 4 * 128 ? (3 * P * K + 3) & ~3 : 4 * 128;
+    return P <= 8 ? 3 * bb_pk(P, K) : 3 * 4 * bb_row(K);
+}
+
+// the level-j sparse table: S_j[i] = max w[i .. i + 2^j - 1], so the maximum
+// over a range of width n, 2^j <= n < 2^(j+1), is exactly
+// max(S_j[lo], S_j[hi + 1 - 2^j]) -- two independent reads.  The host encodes
+// every (entry, pair) range as that query (bb_query, tdoa_capi.cpp: offset of
+// the first window from the scores, distance of the second); a window never
+// crosses its pair's row, both lie inside [lo, hi].  Tables with a range wider
+// than 15 lags take the exhaustive k_grid (kp.bb_wide; configs 3 / 4: <= 11 / 15).
+template <typename T>
+__device__ __forceinline__ T bb_range_max(const T *Wl, uint32_t q)
+{
+    const int o1 = (int)(q & 0x1FFFu), dl = (int)(q >> 13);
+    return vmax<T>(Wl[o1], Wl[o1 + dl]);
 }
 
 // One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
-// by this wave before the call); M8: bb_scratch(P, K) LDS scratch elements of
-// this wave (16-B aligned);
-// tiles / rng: the entry table (LDS or global).  Returns the max L (best) and
+// by this wave before the call), followed by bb_scratch(P, K) scratch
+// elements (16-B aligned); qt: the entries' range queries [NT][P];
+// tiles: the entry table (LDS or global).  Returns the max L (best) and
 // its tuple index in first-cell order (bu, INT_MAX when no L exceeded the
 // lowest value).  Every lane returns the same pair.
 template <typename T, int TWC, int JT>
-__device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, T *M8,
-                                           const int32_t *tiles, const uint16_t *rng, int lane,
-                                           T &best_out, int &bu_out, unsigned long long (&bbacc)[8])
+__device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const int32_t *tiles,
+                                           const uint16_t *qt, int lane, T &best_out, int &bu_out,
+                                           unsigned long long (&bbacc)[8])
 {
     (void)bbacc;
     BB_T0();
-    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW;
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW, PKp = bb_pk(P, K);
     const T low = lowest<T>();
     // entry bounds, lane-strided, in L's own pair order
     T bt[JT];
@@ -153,15 +172,11 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
     for (int j = 0; j < JT; j++)
         bt[j] = (lane + 64 * j < NT) ? (T)0 : low;
     if (P <= 8) {
-        // few pairs: a sparse table of the frame's scores -- level j holds
-        // max w[i .. i + 2^j - 1] (j = 1, 2, 3 in M8) -- so the maximum over a
-        // range of width n is exactly max(Sj[lo], Sj[hi + 1 - 2^j]) with 2^j <= n
-        // < 2^(j+1) (n >= 16: plus level-3 windows between): two independent
-        // reads per entry and pair instead of n dependent ones (the range loop:
-        // 69 % of a config-3 wave).  A window that crosses into the next row
-        // is never read: both windows lie inside [lo, hi].
+        // few pairs: levels 1, 2, 3 of every pair in three wave-synced passes
+        // (the range loop they replace issued n dependent reads per range: 69 %
+        // of a config-3 wave)
         const int PK = P * K;
-        T *S2 = M8, *S4 = M8 + PK, *S8 = M8 + 2 * PK;
+        T *S2 = Wl + PKp, *S4 = S2 + PKp, *S8 = S4 + PKp;
         for (int i = lane; i < PK; i += 64)
             S2[i] = vmax<T>(Wl[i], Wl[i + 1 < PK ? i + 1 : i]);
         wave_lds_sync();
@@ -177,17 +192,9 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             if (t < NT) {
                 T mp[8];
 #pragma unroll
-                for (int p = 0; p < 8; p++) {
-                    if (p < P) {
-                        const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8, n = hi - lo + 1;
-                        const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
-                        const T *L = lv ? M8 + (lv - 1) * PK + p * K : Wl + p * K;
-                        T m = vmax<T>(L[lo], L[hi + 1 - (1 << lv)]);
-                        for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
-                            m = vmax<T>(m, L[k]);
-                        mp[p] = m;
-                    }
-                }
+                for (int p = 0; p < 8; p++)
+                    if (p < P)
+                        mp[p] = bb_range_max<T>(Wl, qt[t * P + p]);
                 T b = 0;
 #pragma unroll
                 for (int p = 0; p < 8; p++)
@@ -197,56 +204,58 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, const T *Wl, 
             }
         }
     } else {
-        // per group of four pairs, the 8-wide running maxima M8[g][k] = max
-        // w[k..min(k + 7, K - 1)]: lane 16 g + q builds k = 8q .. 8q + 7 of pair
-        // p0 + g from 15 reads (suffix / prefix maxima, two 16-B stores); then a
-        // range of width <= 16 is max(M8[lo], M8[max(lo, hi - 7)]) -- two reads
-        // per entry and pair, and two wave syncs per four pairs (one pair per
-        // sync, eight reads per element, bound the pass on LDS issue before:
-        // config 4 109.7 -> 108.3 ms per step)
-        const int gq = lane >> 4, q8 = 8 * (lane & 15);
+        // many pairs: the same levels, four pairs per wave sync (all P pairs'
+        // levels would take 3 P K scratch elements per wave: occupancy).  Lane
+        // 16 g + q builds lags k = 8q .. 8q + 7 of pair p0 + g at levels 1, 2, 3
+        // from 15 reads (14 + 12 + 8 maxima, six 16-B stores).  Round 2's
+        // 8-wide maxima alone answered ranges narrower than 8 with
+        // max w[lo .. lo + 7] -- valid but loose bounds: 3.03 entry evaluations
+        // per config-4 frame against 1.87 with exact ones
+        const int RW = bb_row(K), gq = lane >> 4, q8 = 8 * (lane & 15);
+        T *G = Wl + PKp;  // [3][4][RW]
         for (int p0 = 0; p0 < P; p0 += 4) {
-            wave_lds_sync();  // the previous group's M8 reads come first
-            if (p0 + gq < P && q8 < K) {
+            wave_lds_sync();  // the previous group's level reads come first
+            if (p0 + gq < P && q8 < RW) {
                 const T *w = Wl + (p0 + gq) * K;
                 T x[15];
 #pragma unroll
                 for (int d = 0; d < 15; d++)
                     x[d] = w[q8 + d < K ? q8 + d : K - 1];
+                // in place, each level stored as soon as it is built (few live values)
+                T *dst = G + gq * RW + q8;
 #pragma unroll
-                for (int d = 6; d >= 0; d--)  // suffix maxima of x[0..7]
+                for (int d = 0; d < 14; d++)
                     x[d] = vmax<T>(x[d], x[d + 1]);
 #pragma unroll
-                for (int d = 9; d < 15; d++)  // prefix maxima of x[8..14]
-                    x[d] = vmax<T>(x[d], x[d - 1]);
-                T o[8];
-                o[0] = x[0];
+                for (int d = 0; d < 8; d++)
+                    dst[d] = x[d];
 #pragma unroll
-                for (int d = 1; d < 8; d++)
-                    o[d] = vmax<T>(x[d], x[7 + d]);
-                T *dst = M8 + gq * 128 + q8;
+                for (int d = 0; d < 12; d++)
+                    x[d] = vmax<T>(x[d], x[d + 2]);
 #pragma unroll
                 for (int d = 0; d < 8; d++)
-                    dst[d] = o[d];
+                    dst[4 * RW + d] = x[d];
+#pragma unroll
+                for (int d = 0; d < 8; d++)
+                    x[d] = vmax<T>(x[d], x[d + 4]);
+#pragma unroll
+                for (int d = 0; d < 8; d++)
+                    dst[8 * RW + d] = x[d];
             }
             wave_lds_sync();
 #pragma unroll
             for (int j = 0; j < JT; j++) {
                 const int t = lane + 64 * j;
                 if (t < NT) {
+                    T mp[4];
 #pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        const int p = p0 + g;
-                        if (p < P) {  // bounds summed in L's own pair order
-                            const T *m8 = M8 + g * 128;
-                            const int r = rng[t * P + p], lo = r & 0xFF, hi = r >> 8;
-                            T m = m8[lo];
-                            for (int k = lo + 8; k + 7 < hi; k += 8)  // ranges wider than 16
-                                m = vmax<T>(m, m8[k]);
-                            m = vmax<T>(m, m8[hi - 7 > lo ? hi - 7 : lo]);
-                            bt[j] += m;
-                        }
-                    }
+                    for (int g = 0; g < 4; g++)
+                        if (p0 + g < P)
+                            mp[g] = bb_range_max<T>(Wl, qt[t * P + p0 + g]);
+#pragma unroll
+                    for (int g = 0; g < 4; g++)
+                        if (p0 + g < P)  // bounds summed in L's own pair order
+                            bt[j] += mp[g];
                 }
             }
         }

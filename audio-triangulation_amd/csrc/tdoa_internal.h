@@ -101,6 +101,8 @@ struct tdoa_kparams {
     const uint16_t *bb_rng;    // [NT][P] lo | hi << 8
     const uint32_t *bb_tuples; // [U][TW] regrouped tuples
     const int32_t *bb_uidx;    // [U] their index in first-cell order
+    const uint16_t *bb_q;      // [NT][P] the ranges as sparse-table queries (bb_query)
+    int32_t bb_wide;           // some range is wider than a query encodes (k_grid instead)
     // DIRECT on the streaming batch read straight from the capture ring (the
     // persistent trigger lists the firing streams and copies nothing): frame f
     // of the batch is stream frame_ids[f]'s samples from ring index
