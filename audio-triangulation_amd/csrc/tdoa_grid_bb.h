@@ -247,11 +247,24 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
             for (int j = 0; j < JT; j++) {
                 const int t = lane + 64 * j;
                 if (t < NT) {
+                    // the group's four queries in one 8-B read (P % 4 == 0: aligned)
+                    uint32_t qg[4];
+                    if ((P & 3) == 0) {
+                        const uint2 qq = *reinterpret_cast<const uint2 *>(qt + t * P + p0);
+                        qg[0] = qq.x & 0xFFFFu;
+                        qg[1] = qq.x >> 16;
+                        qg[2] = qq.y & 0xFFFFu;
+                        qg[3] = qq.y >> 16;
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < 4; g++)
+                            qg[g] = p0 + g < P ? qt[t * P + p0 + g] : 0u;
+                    }
                     T mp[4];
 #pragma unroll
                     for (int g = 0; g < 4; g++)
                         if (p0 + g < P)
-                            mp[g] = bb_range_max<T>(Wl, qt[t * P + p0 + g]);
+                            mp[g] = bb_range_max<T>(Wl, qg[g]);
 #pragma unroll
                     for (int g = 0; g < 4; g++)
                         if (p0 + g < P)  // bounds summed in L's own pair order
@@ -275,30 +288,45 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
 
     T best = low;
     int bu = INT_MAX;
-    // evaluate one entry: one tuple per lane; only L > lowest is recorded (the
-    // exhaustive scan never records an L equal to its start value)
-    auto eval = [&](int t) {
-        BB_COUNT(4);
-        const int start = tiles[2 * t], cnt = tiles[2 * t + 1];
-        T L = low;
-        int ui = INT_MAX;
-        if (lane < cnt) {
+    // an entry's evaluation in two halves: fetch (its tuple words and indices,
+    // one tuple per lane, from L2) and consume (the gathers, L, the wave's
+    // best).  Only L > lowest is recorded (the exhaustive scan never records an
+    // L equal to its start value).
+    struct Pre {
+        uint32_t w[TWC];
+        int ui, cnt;
+    };
+    auto fetch = [&](int t, Pre &pr) {
+        const int start = tiles[2 * t];
+        pr.cnt = tiles[2 * t + 1];
+        pr.ui = INT_MAX;
+        if (lane < pr.cnt) {
             const int u = start + lane;
+#pragma unroll
+            for (int tw = 0; tw < TWC; tw++)
+                if (tw < TW)
+                    pr.w[tw] = kp.bb_tuples[(size_t)u * TW + tw];
+            pr.ui = kp.bb_uidx[u];
+        }
+    };
+    auto consume = [&](const Pre &pr) {
+        BB_COUNT(4);
+        T L = low;
+        if (lane < pr.cnt) {
             L = 0;
 #pragma unroll
             for (int tw = 0; tw < TWC; tw++) {
                 if (tw < TW) {
-                    const uint32_t word = kp.bb_tuples[(size_t)u * TW + tw];
 #pragma unroll
                     for (int b = 0; b < 4; b++) {
                         const int p = 4 * tw + b;
                         if (p < P)
-                            L += Wl[p * K + ((word >> (8 * b)) & 0xFFu)];
+                            L += Wl[p * K + ((pr.w[tw] >> (8 * b)) & 0xFFu)];
                     }
                 }
             }
-            ui = kp.bb_uidx[u];
         }
+        const int ui = pr.ui;
         const bool win = L > low && (L > best || (L == best && ui < bu));
         if (__ballot(win) == 0)
             return;
@@ -308,19 +336,58 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
         best = v;
         bu = vi;
     };
-    if (NT > 0)
-        eval(seed);
+    Pre pa, pb;
+    if (NT > 0) {
+        fetch(seed, pa);
+        consume(pa);
+    }
     BB_MARK(2);
+    // the other entries whose bound is not below the best, in entry order,
+    // software-pipelined by one: the next candidate's words are in flight
+    // while this one is consumed (the buffers alternate: a register copy of a
+    // pending load would wait for it).  A candidate is re-checked against the
+    // best before it is consumed -- the best may have risen since.
+    uint64_t mk[JT];
 #pragma unroll
-    for (int j = 0; j < JT; j++) {
-        const int t = lane + 64 * j;
-        uint64_t mask = __ballot(t < NT && t != seed && !(bt[j] < best));
-        while (mask) {
-            const int l = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            if (!(readlane(bt[j], l) < best))  // the best may have risen since
-                eval(l + 64 * j);
+    for (int j = 0; j < JT; j++)
+        mk[j] = __ballot(lane + 64 * j < NT && lane + 64 * j != seed && !(bt[j] < best));
+    auto pop = [&]() -> int {  // straight-line (an early return indexed mk in scratch)
+        int r = -1;
+#pragma unroll
+        for (int j = 0; j < JT; j++) {
+            const bool take = r < 0 && mk[j] != 0;
+            if (take)
+                r = __builtin_ctzll(mk[j]) + 64 * j;
+            mk[j] = take ? mk[j] & (mk[j] - 1) : mk[j];
         }
+        return r;
+    };
+    auto bound_of = [&](int t) -> T {
+        T b = low;
+#pragma unroll
+        for (int j = 0; j < JT; j++)
+            if ((t >> 6) == j)
+                b = readlane(bt[j], t & 63);
+        return b;
+    };
+    int cur = pop();
+    if (cur >= 0)
+        fetch(cur, pa);
+    while (cur >= 0) {
+        int nx = pop();
+        if (nx >= 0)
+            fetch(nx, pb);
+        if (!(bound_of(cur) < best))
+            consume(pa);
+        cur = nx;
+        if (cur < 0)
+            break;
+        nx = pop();
+        if (nx >= 0)
+            fetch(nx, pa);
+        if (!(bound_of(cur) < best))
+            consume(pb);
+        cur = nx;
     }
     BB_MARK(3);
     best_out = best;
