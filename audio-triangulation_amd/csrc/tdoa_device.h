@@ -33,20 +33,57 @@ __device__ __forceinline__ uint4 frame_chunk(const tdoa_kparams &kp, const int16
     return reinterpret_cast<const uint4 *>(frames + row * kp.N)[k];
 }
 
-// the same chunk of mic m of streaming slot `slot`, straight from the capture
-// ring (kp.frame_ring; dma_sampler.c:17-23 round-robin bytes): samples
-// ring_at + 8k + i (wrapping at ring_len), zero before the stream's first
-// sample -- the bytes the trigger scanned (k_stream_trigger_p)
-__device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, int64_t slot, int m, int k)
+// a streaming slot's frame in the capture ring (kp.frame_ring): its stream's
+// bytes (dma_sampler.c:17-23 round-robin), the absolute index of the frame's
+// first sample and that sample's ring index
+struct RingSlot {
+    const uint8_t *cap;
+    int64_t t0, j;
+};
+__device__ __forceinline__ RingSlot ring_slot(const tdoa_kparams &kp, int64_t slot)
+{
+    RingSlot r;
+    r.cap = kp.frame_ring + (size_t)kp.frame_ids[slot] * kp.ring_len * kp.M;
+    r.t0 = kp.frame_end[slot] - kp.N;
+    r.j = kp.frame_ring_at[slot];
+    return r;
+}
+
+// chunk k (8 samples) of mic m of that frame: samples j + 8k + i (wrapping at
+// ring_len), zero before the stream's first sample -- the bytes the trigger
+// scanned (k_stream_trigger_p)
+__device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, const RingSlot &rs, int m, int k)
 {
     const int M = kp.M;
     const int64_t cl = kp.ring_len;
-    const uint8_t *cap = kp.frame_ring + (size_t)kp.frame_ids[slot] * cl * M + m;
-    const int64_t t0 = kp.frame_end[slot] - kp.N + 8 * k;  // absolute index of sample 8k
-    int64_t j = kp.frame_ring_at[slot] + 8 * k;
+    const uint8_t *cap = rs.cap + m;
+    const int64_t t0 = rs.t0 + 8 * k;  // absolute index of sample 8k
+    int64_t j = rs.j + 8 * k;
     if (j >= cl)
         j -= cl;
     uint32_t b[8];
+    if (M == 3 && t0 >= 0 && j + 10 <= cl) {  // the 28 bytes read stay in the ring
+        // three mics (config 5): the 22 bytes holding the chunk in two wide
+        // loads (7 aligned dwords), shifted to the sample's byte, then every
+        // third byte (eight byte loads per chunk bound the staging on the
+        // texture units)
+        const uintptr_t a = (uintptr_t)(cap + j * 3);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3u);
+        uint32_t w[7];
+#pragma unroll
+        for (int d = 0; d < 7; d++)
+            w[d] = wp[d];
+        uint32_t x[6];
+#pragma unroll
+        for (int d = 0; d < 6; d++)
+            x[d] = __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh);
+        // sample i is byte 3i of x: 0, 3 | 6, 9 | 12, 15 | 18, 21
+        return make_uint4(__builtin_amdgcn_perm(0u, x[0], 0x0C030C00u),
+                          __builtin_amdgcn_perm(x[2], x[1], 0x0C050C02u),
+                          __builtin_amdgcn_perm(x[3], x[3], 0x0C030C00u),
+                          __builtin_amdgcn_perm(x[5], x[4], 0x0C050C02u));
+    }
     if (t0 >= 0 && j + 8 <= cl) {
 #pragma unroll
         for (int i = 0; i < 8; i++)
@@ -61,6 +98,11 @@ __device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, int64_t slot
     return make_uint4(b[0] | b[1] << 16, b[2] | b[3] << 16, b[4] | b[5] << 16, b[6] | b[7] << 16);
 }
 
+
+__device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, int64_t slot, int m, int k)
+{
+    return ring_chunk(kp, ring_slot(kp, slot), m, k);
+}
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 

@@ -58,6 +58,7 @@ __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
+    DIAG_STAMP(10);
     if (count) {  // batch size known on the device only (streaming pipeline)
         const int64_t c = *count;
         B = c < B ? c : B;
@@ -490,6 +491,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
+    DIAG_STAMP(10);
     if (count) {  // batch size known on the device only (streaming pipeline)
         const int64_t c = *count;
         if constexpr (EMA)

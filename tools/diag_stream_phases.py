@@ -44,6 +44,9 @@ for nm, a, b in names:
     d = st[:, b] - st[:, a]
     print(f"  {nm:14s} median {np.median(d):9.0f} cyc  ({np.median(d) / np.median(tot) * 100:5.1f}%)")
 print(f"  total          median {np.median(tot):9.0f} cyc")
+print("  before stage: count read %d cyc; stage split: issue+zero %d, frame data+row sums %d, prep+stores %d (median)" %
+      (np.median(st[:, 0] - st[:, 10]), np.median(st[:, 6] - st[:, 0]), np.median(st[:, 7] - st[:, 6]),
+       np.median(st[:, 1] - st[:, 7])))
 print("  grid split: scan %d, reductions %d, final %d cyc (median)" %
       (np.median(st[:, 8] - st[:, 4]), np.median(st[:, 9] - st[:, 8]), np.median(st[:, 5] - st[:, 9])))
 t0 = st[:, 0] - st[:, 0].min()
