@@ -283,6 +283,10 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
     const long long thr = (long long)2 << (2 * hb);  // POWER_THRESHOLD, sample_compute.h:21
     for (int64_t sb = s0; sb < S; sb += GW, s += GW) {
         const bool have = s < S;
+        // a stream that fired during the previous hop cannot fire in this one
+        // (its ring holds fewer than N samples for every candidate: a >= amin
+        // >= H); ~1 in 5 streams at config 5: no scan
+        const bool skip = __builtin_amdgcn_readfirstlane((int)(!have || rs + N - pos - 1 >= H)) != 0;
         const uint8_t *cap = sp.capture + (size_t)(have ? s : 0) * cl * M;
         uint32_t x[3][CW];
 #pragma unroll
@@ -318,6 +322,10 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
         if (sn < S) {
             fetch(sn, wc, shc);
             rsn = sp.ring_start[sn];
+        }
+        if (skip) {
+            rs = rsn;
+            continue;
         }
         auto smp = [&](int r, int i, int m) -> int {
             const int b = i * M + m;
