@@ -234,7 +234,7 @@ def test_grid_exact_on_own_scores(phat3, kind):
     assert (got["max_Lf"] == mx).all()
 
 
-@pytest.mark.parametrize("shape", ["cfg3", "cfg4"])
+@pytest.mark.parametrize("shape", ["cfg3", "cfg4", "wide"])
 @pytest.mark.parametrize("kind", ["adc", "noise_only", "constant"])
 def test_grid_bb_exact_on_own_scores(shape, kind):
     """Configs 3/4 solve the grid by exact branch and bound (k_grid_bb: entries
@@ -242,8 +242,11 @@ def test_grid_bb_exact_on_own_scores(shape, kind):
     below the best L found).  Cell and max L must equal the exhaustive float32
     scan of the engine's own weighted scores bit for bit: peaked scores (ADC
     frames, strong pruning), flat noisy scores (weak bounds) and all-equal
-    scores (every entry ties: first cell)."""
-    M, N, xy = (4, 4096, synth.square_mics(0.15)) if shape == "cfg3" else (8, 2048, synth.circle_mics(8, 0.15))
+    scores (every entry ties: first cell).  "wide": a 0.3 m square, whose
+    entries span lag ranges wider than the sparse-table queries encode (> 15
+    lags): the table is marked wide and the exhaustive k_grid solves it."""
+    M, N, xy = {"cfg3": (4, 4096, synth.square_mics(0.15)), "cfg4": (8, 2048, synth.circle_mics(8, 0.15)),
+                "wide": (4, 2048, synth.square_mics(0.3))}[shape]
     loc = Localizer(engine="gcc_phat", num_mics=M, frame_len=N, mic_xy=xy)
     lut = loc.lut()
     B = 300
