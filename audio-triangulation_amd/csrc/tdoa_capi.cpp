@@ -330,6 +330,8 @@ uint16_t bb_query(int P, int K, int p, int lo, int hi)
         o1 = lv * PKp + p * K + lo;  // levels [3][P][K] after the scores
     else
         o1 = PKp + (lv - 1) * 4 * RW + (p & 3) * RW + lo;  // [3][4][RW]: four pairs a group
+    if (o1 < 0 || o1 >= 0x1FFF)
+        return 0x1FFF;  // the offset does not fit 13 bits: wide (exhaustive k_grid)
     return (uint16_t)(o1 | ((n - (1 << lv)) << 13));
 }
 

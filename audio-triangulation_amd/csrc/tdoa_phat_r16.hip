@@ -500,11 +500,17 @@ __device__ __forceinline__ const char *kernarg_base()
     asm volatile("" : "+s"(k));
     return k;
 }
+// The offset below holds only while both structs are 8-byte aligned and
+// (kp, out) stay k_frame16's first two parameters.
+static_assert(alignof(tdoa_kparams) <= 8 && alignof(tdoa_kout) == 8,
+              "kernarg_out(): tdoa_kout must sit at sizeof(tdoa_kparams) rounded to 8");
 __device__ __forceinline__ const tdoa_kout *kernarg_out()
 {
     return reinterpret_cast<const tdoa_kout *>(kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
 }
 
+// (kp, out) must stay the first two parameters: kernarg_out() reads `out`
+// at its kernarg offset
 template <int C, int M>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, int64_t B,

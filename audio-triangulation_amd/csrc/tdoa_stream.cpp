@@ -215,8 +215,14 @@ extern "C" int tdoa_stream_step(tdoa_stream *st, const tdoa_stream_outputs *out,
     const int par = (int)(st->hop & 1);
     if (!st->use_graph || !s) {
         const int rc = enqueue_step(st, out, s, par);
-        if (!rc)
+        if (!rc) {
             st->hop++;
+        } else {
+            // a launch after the trigger failed: the trigger may have counted
+            // into this hop's slot without the hop advancing; both slots are
+            // zeroed so the next hop's slot base starts at 0 again
+            (void)hipMemsetAsync(st->sp.count, 0, 2 * sizeof(int32_t), s);
+        }
         return rc;
     }
     const tdoa_stream_outputs want = out ? *out : tdoa_stream_outputs{};

@@ -178,11 +178,15 @@ __global__ void __launch_bounds__(TPB) k_stream_trigger(tdoa_stream_params sp)
     if (tid == 0) {
         slot = atomicAdd(sp.count, 1);
         const int64_t end = pos + 1 + a;
-        sp.ids[slot] = (int32_t)s;
-        sp.end[slot] = end;
+        if (slot < (int)gridDim.x) {  // one slot per stream (see k_stream_trigger_p)
+            sp.ids[slot] = (int32_t)s;
+            sp.end[slot] = end;
+        }
         sp.ring_start[s] = end;
     }
     __syncthreads();
+    if (slot >= (int)gridDim.x)
+        return;
     // the frame as 8-bit samples (the capture's values; DIRECT widens them,
     // kp.frames_u8), four per dword store
     uint32_t *dst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(sp.frames) + (size_t)slot * M * N);
@@ -448,7 +452,9 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
     int o = slot_base;
     for (int w = 0; w < wv; w++)
         o += nfired[w];
-    if (lane < my_n) {
+    // o + lane < S always holds while the hop's slot started at 0 (one slot per
+    // firing stream); the clamp keeps a corrupted counter from writing past S
+    if (lane < my_n && o + lane < S) {
         sp.ids[o + lane] = my_id;
         sp.end[o + lane] = my_end;
         sp.ring_at[o + lane] = my_at;

@@ -112,15 +112,23 @@ def sum_over_ranks(xs, device=None) -> list[float]:
 
 
 def timed(step, steps: int, warmup: int, sync=lambda: None, device=None,
-          on_start=None, on_end=None) -> dict:
+          on_start=None, on_end=None, barrier_fn=None) -> dict:
     """The bench contract's timed region: `warmup` untimed calls of step(k),
     then EXACTLY `steps` calls bracketed by sync + barrier + sync on both
-    sides; the wall time is the max over ranks.  on_start / on_end run right
-    inside the bracket (e.g. HIP event records on the launch stream)."""
+    sides; the job time is the max over ranks.  on_start / on_end run right
+    inside the bracket (e.g. HIP event records on the launch stream).
+
+    The start is barrier-aligned (every rank leaves the opening barrier
+    together); each rank's clock stops right after its OWN closing sync, before
+    the closing barrier, so the barrier's RCCL round trip is not part of any
+    rank's time.  max over ranks then still is the slowest rank's end: the
+    whole-job time for frames that are independent (sample_compute.h:105-139).
+    `barrier_fn` replaces the process-group barrier (tests inject a slow one)."""
+    bar = barrier_fn or barrier
     for k in range(warmup):
         step(k)
     sync()
-    barrier()
+    bar()
     sync()
     t0 = time.perf_counter()
     if on_start:
@@ -130,9 +138,9 @@ def timed(step, steps: int, warmup: int, sync=lambda: None, device=None,
     if on_end:
         on_end()
     sync()
-    barrier()
+    wall = time.perf_counter() - t0  # this rank's own end
+    bar()
     sync()
-    wall = time.perf_counter() - t0
     return {"wall_s": wall, "wall_max_s": max_over_ranks(wall, device)}
 
 

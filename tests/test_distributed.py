@@ -46,6 +46,18 @@ def _worker(rank, world, port, q):
         done = []
         t = shard.timed(lambda k: done.append(O.localize_batch(frames[lo:hi], 46, win, lut)),
                         steps=3, warmup=1)
+        # the closing barrier is outside every rank's clock: a barrier that
+        # sleeps 50 ms on its second (closing) call must not show in wall_max_s
+        calls = []
+
+        def slow_barrier():
+            calls.append(1)
+            if len(calls) == 2:
+                import time
+                time.sleep(0.05)
+            shard.barrier()
+
+        ts = shard.timed(lambda k: None, steps=3, warmup=0, barrier_fn=slow_barrier)
         total = shard.sum_over_ranks([(hi - lo) * 3])[0]
         mx = shard.max_over_ranks(float(rank + 1))
         cfg4 = bench.CONFIGS[4]
@@ -55,7 +67,8 @@ def _worker(rank, world, port, q):
         seeds = [shard.frame_seed(0x5EED0002, ri.rank, r) for r in range(3)]
         out = {"rank": rank, "ranks_seen": shard.ranks_seen(), "wall": t["wall_s"],
                "wall_max": t["wall_max_s"], "steps_done": len(done), "total": total, "max": mx,
-               "per4": per4, "per2": per2, "seeds": seeds}
+               "per4": per4, "per2": per2, "seeds": seeds, "slow_wall_max": ts["wall_max_s"],
+               "slow_calls": len(calls)}
         if rank == 0:
             full = O.localize_batch(frames, 46, win, lut)
             out["ok"] = all((res[k] == full[k]).all() for k in ("lags", "gate", "cell", "xy"))
@@ -87,6 +100,9 @@ def test_two_rank_gloo_bench_rank_logic():
     assert rs[0]["per4"] + rs[1]["per4"] == 1_000_000           # config 4: one global batch
     assert rs[0]["per2"] == rs[1]["per2"] == 4096               # config 2: per-GPU batch
     assert len(set(rs[0]["seeds"] + rs[1]["seeds"])) == 6       # distinct frames per rank/batch
+    # the closing barrier (slept 50 ms) is not inside the timed window
+    assert all(r["slow_calls"] == 2 for r in rs)
+    assert all(r["slow_wall_max"] < 0.04 for r in rs), [r["slow_wall_max"] for r in rs]
 
 
 def test_shard_range_covers_everything_once():

@@ -14,6 +14,7 @@
 #                         per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
 #   ablib[:L1,L2,..]      bench config 2 once per library tdoa/<L>.so (TDOA_LIB)
 #   testlib:L[:FILES]     pytest -m gpu against tdoa/<L>.so
+#   calib                 tools/hbm_copy (achievable HBM), plain and under rocprofv3
 #   smoke                 __graft_entry__.smoke()
 #
 # Env: TAG (output subdirectory, default "cur"), STEPS (bench steps),
@@ -106,6 +107,17 @@ for step in "$@"; do
         PARGS="--config $c --engine $e --steps 24 --warmup 2 --no-cpu $BENCH_ARGS"
         prof "${n}_c${c}_$e" --pmc ${ctr//,/ } || exit 29
         echo "pmcx $n c$c $e done"
+        ;;
+    calib)
+        # achievable HBM: tools/hbm_copy (16-B-per-lane copy + read sweeps, 1 GiB
+        # buffers) plain, then under rocprofv3 --kernel-trace --stats
+        timeout -k 10 120 "$ROOT/tools/hbm_copy" 1024 20 > "$OUT/calib.json" 2> "$OUT/calib.err" \
+            || { cat "$OUT/calib.err"; exit 30; }
+        cat "$OUT/calib.json"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/calib_kt" -o run \
+            --output-format csv -- "$ROOT/tools/hbm_copy" 1024 20 > "$ROOT/$OUT/calib_kt.log" 2>&1) \
+            || { tail -5 "$OUT/calib_kt.log"; exit 31; }
+        cut -d, -f1-4,6 "$OUT/calib_kt/run_kernel_stats.csv" | head -5
         ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
