@@ -207,6 +207,7 @@ struct tdoa_ctx {
     int32_t *d_tuple_cell = nullptr;
     float *d_tw = nullptr;  // GCC_PHAT twiddles: [N] e^{-2 pi i k/N}, then [N+1] e^{-2 pi i k/2N}
     void *d_p1k_img = nullptr;  // LDS table image of the config-2 GCC_PHAT kernel
+    void *d_w64_img = nullptr;  // ... and of its one-frame-per-wave form
     // weighted-score scratch for the grid kernel when the caller did not ask
     // for weighted scores ([B][P][K] int64 or float); grows on demand
     void *d_wscratch = nullptr;
@@ -406,6 +407,8 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_p1k_img);
     c->d_p1k_img = nullptr;
+    (void)hipFree(c->d_w64_img);
+    c->d_w64_img = nullptr;
     (void)hipFree(c->d_wscratch);
     (void)hipFree(c->d_rscratch);
     (void)hipFree(c->d_cscratch);
@@ -668,6 +671,17 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             }
             kp.p1k_img = c->d_p1k_img;
             kp.p1k_img_bytes = (int32_t)img.size();
+        }
+        tdoa_p1k_w64_image(M, N, c->K, c->U, c->win.data(), c->prior.data(), c->tuples.data(), img);
+        if (!img.empty()) {
+            if (hipMalloc(&c->d_w64_img, img.size()) != hipSuccess ||
+                hipMemcpy(c->d_w64_img, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                free_device(c);
+                delete c;
+                return fail(TDOA_ERR_NOMEM, "uploading the GCC_PHAT (w64) table image failed");
+            }
+            kp.w64_img = c->d_w64_img;
+            kp.w64_img_bytes = (int32_t)img.size();
         }
         if (tdoa_gcc_phat_needs_split(M, N)) {
             const size_t want = (size_t)128 << 20;

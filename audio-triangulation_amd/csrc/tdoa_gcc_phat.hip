@@ -3,6 +3,12 @@
 // float64 oracle, unlike DIRECT whose float steps must round like the
 // reference's IEEE host build.
 #include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#ifndef TDOA_P1K_DEFAULT_W64
+#define TDOA_P1K_DEFAULT_W64 0
+#endif
 #include <stdint.h>
 
 #include <climits>
@@ -665,6 +671,21 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp);
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
                          int64_t B, float phat_eps, void *stream);
 
+// one frame per 64-lane wave (tdoa_p1k_w64.hip)
+bool tdoa_p1k_w64_fits(const tdoa_kparams &kp);
+int tdoa_launch_p1k_w64(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+                        float phat_eps, void *stream);
+// config-2 kernel choice: TDOA_P1K=lean | w64 (A/B runs), else the default
+static bool use_w64(const tdoa_kparams &kp)
+{
+    static const int pick = [] {
+        const char *e = getenv("TDOA_P1K");
+        return e && !strcmp(e, "w64") ? 1 : (e && !strcmp(e, "lean") ? 0 : -1);
+    }();
+    const bool want = pick < 0 ? TDOA_P1K_DEFAULT_W64 : pick == 1;
+    return want && tdoa_p1k_w64_fits(kp);
+}
+
 bool tdoa_phat_r16_fits(int M, int N, int S);
 int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                          float phat_eps, void *scratch, size_t scratch_bytes, void *stream);
@@ -703,6 +724,8 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
     if (!kp.tw || !kp.tw2)
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
+    if (use_w64(kp))
+        return tdoa_launch_p1k_w64(kp, out, frames, B, phat_eps, stream);
     if (tdoa_phat1024_fits(kp))
         return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
     // frame_len 2048 / 4096 with M > 3 or N > 2048: register-pass kernels

@@ -93,6 +93,8 @@ struct tdoa_kparams {
     const uint8_t *lut;        // [P][G] lag index per cell (heat map)
     const void *p1k_img;       // config-2 GCC-PHAT kernel: its LDS table image (16-B units)
     int32_t p1k_img_bytes;
+    const void *w64_img;       // ... and of its one-frame-per-wave form (k_p1k_w64)
+    int32_t w64_img_bytes;
     // exact branch-and-bound grid (k_grid_bb): the distinct tuples regrouped
     // by the 8 x 8-cell tile of their first cell (<= 64 tuples per entry);
     // per entry and pair the lag range [lo, hi] of its tuples
@@ -223,6 +225,9 @@ bool tdoa_gcc_phat_needs_split(int M, int N);
 // Q15 window, lag prior and distinct lag tuples; empty if the shape differs
 void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
                          const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img);
+// the one-frame-per-wave config-2 kernel (tdoa_p1k_w64.hip): its image
+void tdoa_p1k_w64_image(int M, int N, int K, int U, const int32_t *win, const float *prior,
+                        const uint32_t *tuples, std::vector<uint8_t> &img);
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
 bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp);
 bool tdoa_gcc_phat_peak3(const tdoa_kparams &kp);

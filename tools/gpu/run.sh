@@ -14,6 +14,7 @@
 #                         per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
 #   ablib[:L1,L2,..]      bench config 2 once per library tdoa/<L>.so (TDOA_LIB)
 #   testlib:L[:FILES]     pytest -m gpu against tdoa/<L>.so
+#   diagw64               phase stamps of k_p1k_w64 (needs the diag library)
 #   calib                 tools/hbm_copy (achievable HBM), plain and under rocprofv3
 #   smoke                 __graft_entry__.smoke()
 #
@@ -59,6 +60,18 @@ for step in "$@"; do
             TDOA_LIB=$ROOT/audio-triangulation_amd/tdoa/$l.so timeout -k 10 240 python bench.py --steps ${STEPS:-400} \
                 --no-cpu $BENCH_ARGS > "$OUT/ablib_$l.log" 2>&1 || { echo "bench $l failed"; tail -5 "$OUT/ablib_$l.log"; exit 21; }
             tail -1 "$OUT/ablib_$l.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$l value %.4g kernel_ms %.4f frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))"
+        done
+        ;;
+    abenv)
+        # bench (config 2 unless BENCH_ARGS) once per value of an env switch,
+        # ROUNDS times interleaved: abenv:VAR:V1,V2
+        var=$(field "$step" 2 TDOA_P1K); vs=$(field "$step" 3 "lean,w64")
+        for r in $(seq 1 "${ROUNDS:-1}"); do
+            for v in ${vs//,/ }; do
+                env "$var=$v" timeout -k 10 240 python bench.py --steps ${STEPS:-400} --no-cpu --no-parity \
+                    $BENCH_ARGS > "$OUT/abenv_${v}_$r.log" 2>&1 || { echo "bench $var=$v failed"; tail -5 "$OUT/abenv_${v}_$r.log"; exit 21; }
+                tail -1 "$OUT/abenv_${v}_$r.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$var=$v value %.4g kernel_us %.2f frac %.4f' % (d['value'], r['kernel_ms']*1e3, r['frac']))"
+            done
         done
         ;;
     testlib)
@@ -118,6 +131,11 @@ for step in "$@"; do
             --output-format csv -- "$ROOT/tools/hbm_copy" 1024 20 > "$ROOT/$OUT/calib_kt.log" 2>&1) \
             || { tail -5 "$OUT/calib_kt.log"; exit 31; }
         cut -d, -f1-4,6 "$OUT/calib_kt/run_kernel_stats.csv" | head -5
+        ;;
+    diagw64)
+        # phase stamps of k_p1k_w64 (libtdoa_diag.so, make -C audio-triangulation_amd diag)
+        timeout -k 10 120 python tools/diag_w64.py > "$OUT/diag_w64.txt" 2>&1 || { tail -5 "$OUT/diag_w64.txt"; exit 32; }
+        cat "$OUT/diag_w64.txt"
         ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
