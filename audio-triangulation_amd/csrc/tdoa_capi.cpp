@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -222,6 +224,8 @@ struct tdoa_ctx {
     std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx | queries
     int bb_wide = 0;              // a range wider than the queries encode: no k_grid_bb
     void *d_bb = nullptr;
+    void *d_wc = nullptr;         // compact weighted-score chunk table (kp.wc_chunks)
+    std::vector<uint32_t> wc_chunks;
     int bb_NT = 0;
     float *d_mic = nullptr;  // [M][2]
     uint8_t *d_lut = nullptr;  // [P][G]
@@ -404,6 +408,8 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_tuples);
     (void)hipFree(c->d_tuple_cell);
     (void)hipFree(c->d_bb);
+    (void)hipFree(c->d_wc);
+    c->d_wc = nullptr;
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_p1k_img);
     c->d_p1k_img = nullptr;
@@ -721,6 +727,37 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         kp.bb_tuples = (const uint32_t *)(b + a2);
         kp.bb_uidx = (const int32_t *)(b + a3);
         kp.bb_q = (const uint16_t *)(b + a3 + ((((size_t)c->U * 4) + 15) & ~(size_t)15));
+        // compact weighted-score layout: per pair the lag range the tuples use
+        // (vga_heatmap.h:68-93: the LUT clamps lags to it), padded to 4 floats
+        std::vector<int> lo(c->P, 255), hi(c->P, -1);
+        for (int u = 0; u < c->U; u++)
+            for (int p = 0; p < c->P; p++) {
+                const int l = (c->tuples[(size_t)u * c->TW + p / 4] >> (8 * (p & 3))) & 0xFF;
+                lo[p] = std::min(lo[p], l);
+                hi[p] = std::max(hi[p], l);
+            }
+        int off = 0;
+        bool ok = c->P <= TDOA_MAX_PAIRS;
+        c->wc_chunks.clear();
+        for (int p = 0; ok && p < c->P; p++) {
+            const int w = hi[p] - lo[p] + 1;
+            ok = w > 0 && off < 65536;
+            if (!ok)
+                break;
+            kp.wc_lo[p] = (uint8_t)lo[p];
+            kp.wc_w[p] = (uint8_t)w;
+            kp.wc_off[p] = (uint16_t)off;
+            for (int j = 0; j < w; j += 4)
+                c->wc_chunks.push_back((uint32_t)(p * c->K + lo[p] + j) | ((uint32_t)std::min(4, w - j) << 16));
+            off += (w + 3) & ~3;
+        }
+        if (ok && hipMalloc(&c->d_wc, c->wc_chunks.size() * 4) == hipSuccess &&
+            hipMemcpy(c->d_wc, c->wc_chunks.data(), c->wc_chunks.size() * 4, hipMemcpyHostToDevice) ==
+                hipSuccess) {
+            kp.wc_CK = off;
+            kp.wc_nch = (int32_t)c->wc_chunks.size();
+            kp.wc_chunks = (const uint32_t *)c->d_wc;
+        }
     }
     *out = c;
     return TDOA_OK;
@@ -827,7 +864,18 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     const size_t pk = (size_t)B * ctx->P * ctx->K * sz;
     const void *weighted = phat ? (const void *)out->weighted_f : (const void *)out->weighted;
     const bool fused_grid = phat ? tdoa_gcc_phat_grid_in_kernel(ctx->kp) : tdoa_direct_fused_grid(ctx->kp);
-    if (grid && !weighted && !fused_grid) {
+    // the per-frame long-frame kernel (k_frame16) can write only the lags the
+    // grid reads, compacted, when k_grid_bb solves the grid (configs 3, 4)
+    const bool compact = grid && !weighted && !fused_grid && phat && tdoa_gcc_phat_peak3(ctx->kp) &&
+                         tdoa_grid_bb_compact(ctx->kp) && !getenv("TDOA_NO_COMPACT");
+    if (compact) {
+        int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, (size_t)B * ctx->kp.wc_CK * sizeof(float), stream,
+                      "weighted-score");
+        if (rc)
+            return rc;
+        k.weighted_c = (float *)ctx->d_wscratch;
+        weighted = ctx->d_wscratch;
+    } else if (grid && !weighted && !fused_grid) {
         // the grid kernel reads the weighted scores back: keep them in scratch
         int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, pk, stream, "weighted-score");
         if (rc)

@@ -18,6 +18,8 @@
 #include <cmath>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "tdoa_internal.h"
 #include "tdoa_grid_bb.h"
 
@@ -182,6 +184,10 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
     __syncthreads();
 
     unsigned long long bbacc[8] = {};
+    if constexpr (std::is_same<T, float>::value)
+        if (out.weighted_c)  // compact scratch: the unused lags of Wl stay defined (never read)
+            for (int e = lane; e < PK; e += 64)
+                Wl[e] = (T)0;
     for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
 #ifdef TDOA_DIAG
         const unsigned long long t_load = __builtin_amdgcn_s_memtime();
@@ -193,6 +199,42 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
             // iteration waited on every load in turn: ~40 HBM round trips a frame);
             // nontemporal, so the streamed scores do not evict the entry tables'
             // tuples from L2 (every evaluation reads them)
+            bool compact = false;
+            if constexpr (std::is_same<T, float>::value)
+                compact = out.weighted_c != nullptr;
+            if (compact) {
+                // compact scratch: 16-B chunks of the used lags, expanded to
+                // Wl[p][K] (lags no tuple uses are never read)
+                typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+                const v4u_t *s4 = reinterpret_cast<const v4u_t *>(out.weighted_c + f * kp.wc_CK);
+                const int nch = kp.wc_nch;
+                for (int b = 0; b < nch; b += 4 * 64) {
+                    v4u_t t[4];
+                    uint32_t dsc[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {  // clamped: unconditional loads
+                        const int c = b + i * 64 + lane;
+                        const int cc = c < nch ? c : nch - 1;
+                        t[i] = __builtin_nontemporal_load(&s4[cc]);
+                        dsc[i] = kp.wc_chunks[cc];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int c = b + i * 64 + lane;
+                        if (c < nch) {
+                            float *d = reinterpret_cast<float *>(Wl) + (dsc[i] & 0xFFFFu);
+                            const int n = (int)(dsc[i] >> 16);
+                            d[0] = __builtin_bit_cast(float, t[i].x);
+                            if (n > 1)
+                                d[1] = __builtin_bit_cast(float, t[i].y);
+                            if (n > 2)
+                                d[2] = __builtin_bit_cast(float, t[i].z);
+                            if (n > 3)
+                                d[3] = __builtin_bit_cast(float, t[i].w);
+                        }
+                    }
+                }
+            } else {
             const T *src = weighted + f * PK;
             const int nv = (int)(((size_t)PK * sizeof(T)) / 16);
             const bool vec = nv > 0 && (((uintptr_t)src | (uintptr_t)Wl) & 15) == 0;
@@ -221,6 +263,7 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
             }
             for (int e = e0 + lane; e < PK; e += 64)
                 Wl[e] = src[e];
+            }
         }
         wave_lds_sync();  // a wave's LDS operations complete in order
 #ifdef TDOA_DIAG
@@ -304,6 +347,13 @@ bool bb_fits(const tdoa_kparams &kp)
            table + ((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 16 <= BB_LDS;
 }
 
+}  // namespace
+// k_grid_bb solves the float grid and can read the compact scratch
+bool tdoa_grid_bb_compact(const tdoa_kparams &kp)
+{
+    return bb_fits<float>(kp) && kp.wc_chunks != nullptr && kp.wc_CK > 0 && kp.wc_nch > 0;
+}
+namespace {
 int hip_fail(hipError_t e, const char *what)
 {
     char buf[256];

@@ -105,6 +105,15 @@ struct tdoa_kparams {
     const int32_t *bb_uidx;    // [U] their index in first-cell order
     const uint16_t *bb_q;      // [NT][P] the ranges as sparse-table queries (bb_query)
     int32_t bb_wide;           // some range is wider than a query encodes (k_grid instead)
+    // compact weighted-score scratch (k_frame16 -> k_grid_bb): per frame only
+    // the lags some grid tuple uses, pair p's lags [wc_lo, wc_lo + wc_w) at
+    // wc_off[p] (a multiple of 4 floats), wc_CK floats per frame; k_grid_bb
+    // expands it in LDS by 16-B chunks: wc_chunks[c] = LDS element of the
+    // chunk's first lag (p * K + lag) | valid floats << 16
+    int32_t wc_CK, wc_nch;
+    uint16_t wc_off[TDOA_MAX_PAIRS];
+    uint8_t wc_lo[TDOA_MAX_PAIRS], wc_w[TDOA_MAX_PAIRS];
+    const uint32_t *wc_chunks;
     // DIRECT on the streaming batch read straight from the capture ring (the
     // persistent trigger lists the firing streams and copies nothing): frame f
     // of the batch is stream frame_ids[f]'s samples from ring index
@@ -140,6 +149,9 @@ struct tdoa_kout {
     // the kernels that keep the scores on chip (k_frame16) instead of scores_f
     // (slots outside the lag range are not written and not read)
     float *peak3;
+    // the compact weighted-score scratch ([B][kp.wc_CK], see tdoa_kparams),
+    // written by k_frame16 and read by k_grid_bb in place of weighted_f
+    float *weighted_c;
 };
 
 // Streaming state of one pipeline (tdoa_stream.hip); all device pointers.
@@ -229,6 +241,8 @@ void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int3
 void tdoa_p1k_w64_image(int M, int N, int K, int U, const int32_t *win, const float *prior,
                         const uint32_t *tuples, std::vector<uint8_t> &img);
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
+// the float grid runs k_grid_bb and can read the compact scratch (tdoa_grid.hip)
+bool tdoa_grid_bb_compact(const tdoa_kparams &kp);
 bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp);
 bool tdoa_gcc_phat_peak3(const tdoa_kparams &kp);
 int tdoa_launch_gcc_phat_split(const tdoa_kparams &kp, const tdoa_kout &out,

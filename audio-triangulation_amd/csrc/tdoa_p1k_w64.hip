@@ -68,7 +68,9 @@ static_assert(IMG_FIXED % 16 == 0, "tuple table must stay 16-B aligned");
 // an instruction offset (< 64 KiB); the tiles follow at W64_TILES.
 constexpr int W64_UMAX = 2560;                    // padded tuple count the layout holds
 constexpr int W64_TILES = IMG_FIXED + W64_UMAX * 4;
-constexpr int W64_LDS_BYTES = W64_TILES + W64_NW * W64_TILE + W64_NW * 4 + W64_NW * 16;  // + balance words, bin 512
+// + words: [16] balance, [16] pair flags, [16][4] pair exchange; then bin 512
+constexpr int W64_WORDS = W64_NW * 6;
+constexpr int W64_LDS_BYTES = W64_TILES + W64_NW * W64_TILE + W64_WORDS * 4 + W64_NW * 16;
 static_assert(W64_LDS_BYTES <= 160 * 1024, "k_p1k_w64 exceeds the CU's LDS");
 
 // residue column held by lane L (0..63): lane pairs (2i, 2i+1) hold partner
@@ -243,6 +245,9 @@ __host__ __device__ constexpr uint32_t w64_lane_info(int L, int w)
                         ((uint32_t)((L & 15) * W64_ROW + 128 * (L >> 4)) << 16);
 }
 
+#ifndef W64_PAIR
+#define W64_PAIR 1  // grid solve of two frames per gather (waves w, w ^ 1)
+#endif
 #ifndef W64_BAL
 #define W64_BAL 2  // issue balance: 0 none, 1 at phase boundaries, 2 also inside the transforms
 #endif
@@ -566,8 +571,10 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
     } while (0)
 #endif
     int *prog = (int *)(tiles + W64_NW * W64_TILE);  // [SIMD group][4], after the tiles
-    if (lane == 0)
+    if (lane == 0) {
         prog[(wave & 3) * 4 + (wave >> 2)] = 0;
+        prog[W64_NW + wave] = 0;  // pair flag (read after the staging barrier)
+    }
     __builtin_amdgcn_s_setprio(2);
     W64Lane W;
     W.prog = prog;
@@ -577,7 +584,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
     W.tile = tiles + __builtin_amdgcn_readfirstlane(wave) * W64_TILE;
     W.img = img;
     W.L8 = 8 * lane;
-    W.b512 = (f2 *)(tiles + W64_NW * W64_TILE + W64_NW * 4) + 2 * __builtin_amdgcn_readfirstlane(wave);
+    W.b512 = (f2 *)(tiles + W64_NW * W64_TILE + W64_WORDS * 4) + 2 * __builtin_amdgcn_readfirstlane(wave);
     auto balance = [&]() {
         if (W64_BAL >= 1)
             w64_balance(W);
@@ -703,6 +710,143 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
         out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
 
     if (do_grid) {
+#if W64_PAIR
+        // ---- grid solve (vga_heatmap.h:99-108), two frames at once: the waves
+        // w and w ^ 1 share one [p][KPAD] f2 table of their weighted scores
+        // (frame of the even wave in .x, of the odd wave in .y) in the even
+        // wave's tile, each gathers half of the distinct lag tuples for both
+        // frames (alternate 256-tuple steps), then they swap partial maxima.
+        // Hand-offs through LDS words of the pair (same CU: in-order DS, no
+        // fence); the odd wave writes only after the even wave has finished
+        // reading its tile.
+        const int odd = wave & 1;
+        volatile int *flag = prog + W64_NW + (wave & ~1);  // [pair][2]: 1 table half written, 2 partials
+        const int toff = (W64_TILES + __builtin_amdgcn_readfirstlane(wave & ~1) * W64_TILE + 1023) & ~1023;
+        float *wsc = (float *)(smem + toff);  // [p][KPAD][2]
+        auto wait_flag = [&](volatile int *fp, int v) {
+            while (__builtin_amdgcn_readfirstlane(*fp) < v)
+                __builtin_amdgcn_s_sleep(1);
+        };
+        wave_lds_sync();  // after the last pair's reads of this wave's tile
+        if (odd)
+            wait_flag(flag, 1);  // the even wave is done with its tile
+        {
+            const int L = W.L8 >> 3;
+            const int q = L >> 4;
+            const int lg = 2 * (L & 15) + ((q & 1) ? -64 : 0) + ((q & 2) ? 32 : 0);
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+                if (lg + c >= -S && lg + c <= S)
+#pragma unroll
+                    for (int p = 0; p < P; p++)
+                        wsc[(p * W64_KPAD + lg + c + S) * 2 + odd] = wv[p][c];
+            if (L < 3)  // lag slot 127 of every pair: the padding tuple
+                wsc[(L * W64_KPAD + W64_KPAD - 1) * 2 + odd] = -INFINITY;
+        }
+        wave_lds_sync();
+        if (lane == 0)
+            flag[odd] = 1;
+        wait_flag(flag + (odd ^ 1), 1);  // the partner's half of the table is written
+        W64_MARK();
+        f2 gv = f2{-INFINITY, -INFINITY};
+        int gs0 = INT_MAX - 64, gs1 = INT_MAX - 64;  // (tuple index - lane) of the lane's best, per frame
+        const char *lds = smem;
+        auto gather = [&](const uint32_t (&qq)[4], f2 (&g)[4][3]) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                g[i][0] = *reinterpret_cast<const f2 *>(lds + ((qq[i] & 0x3FFu) | toff));
+                g[i][1] = *reinterpret_cast<const f2 *>(lds + (((qq[i] >> 10) & 0x3FFu) | toff) + W64_KPAD * 8);
+                g[i][2] = *reinterpret_cast<const f2 *>(lds + ((qq[i] >> 20) | toff) + 2 * W64_KPAD * 8);
+            }
+        };
+        auto consume = [&](const f2 (&gg)[4][3], int ub) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const f2 Lg = (gg[i][0] + gg[i][1]) + gg[i][2];
+                if (Lg.x > gv.x) {
+                    gv.x = Lg.x;
+                    gs0 = ub + 64 * i;
+                }
+                if (Lg.y > gv.y) {
+                    gv.y = Lg.y;
+                    gs1 = ub + 64 * i;
+                }
+            }
+        };
+        // this wave's steps: u = 256 (2 j + odd), pipelined by one step
+        uint32_t qa[4];
+        f2 ga[4][3];
+        const int nst = Upad / 256;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            qa[i] = tups[256 * odd + 64 * i + lane];
+        gather(qa, ga);
+        for (int st = odd; st < nst; st += 2) {
+            const int sn = st + 2 < nst ? st + 2 : st;  // (a harmless re-read)
+            uint32_t qn[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                qn[i] = tups[256 * sn + 64 * i + lane];
+            f2 gn[4][3];
+            gather(qn, gn);
+            consume(ga, 256 * st);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                qa[i] = qn[i];
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    ga[i][p] = gn[i][p];
+            }
+        }
+        W64_MARK();
+        // (max L, first tuple) per frame over the wave, each lane's candidate
+        // cell requested before the reductions
+        int gu[2] = {gs0 + lane, gs1 + lane}, cell2[2];
+        float mv[2] = {gv.x, gv.y};
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int myu = gu[j];
+            const int mycell = kp.tuple_cell[(myu < 0 || myu >= kp.U) ? 0 : myu];
+            int gk = fkey(mv[j]);
+            wave_argmax_key(gk, gu[j]);
+            mv[j] = fkey_value(gk);
+            const uint64_t wm = __ballot(myu == gu[j] && gu[j] >= 0 && gu[j] < kp.U);
+            cell2[j] = wm ? __builtin_amdgcn_readlane(mycell, __builtin_ctzll(wm)) : kp.tuple_cell[0];
+        }
+        // swap partials: each wave needs the partner's result for its own frame
+        int *xch = prog + 2 * W64_NW + 4 * wave;  // [wave][3]: key, index, cell for the partner's frame
+        if (lane == 0) {
+            xch[0] = fkey(mv[odd ^ 1]);
+            xch[1] = gu[odd ^ 1];
+            xch[2] = cell2[odd ^ 1];
+        }
+        wave_lds_sync();
+        if (lane == 0)
+            flag[odd] = 2;
+        wait_flag(flag + (odd ^ 1), 2);
+        const volatile int *px = prog + 2 * W64_NW + 4 * (wave ^ 1);
+        const int ok_ = __builtin_amdgcn_readfirstlane(px[0]), oi = __builtin_amdgcn_readfirstlane(px[1]),
+                  oc = __builtin_amdgcn_readfirstlane(px[2]);
+        int mk = fkey(mv[odd]), mi = gu[odd], cell = cell2[odd];
+        if (ok_ > mk || (ok_ == mk && oi < mi)) {
+            mk = ok_;
+            mi = oi;
+            cell = oc;
+        }
+        const float gvf = fkey_value(mk);
+        if (live && lane == 0) {
+            if (out.cell)
+                out.cell[f] = cell;
+            if (out.max_Lf)
+                out.max_Lf[f] = gvf;
+            if (out.xy) {
+                const int cx = cell % kp.grid_W, cy = cell / kp.grid_W;
+                out.xy[2 * f] = (float)(cx - kp.half_w) / kp.grid_scale;
+                out.xy[2 * f + 1] = (float)(kp.half_h - cy) / kp.grid_scale;
+            }
+        }
+        W64_MARK();
+#else
         // ---- grid solve (vga_heatmap.h:99-108) of the wave's frame: weighted
         // scores [p][KPAD] f32 in the wave's tile, lanes split the distinct lag
         // tuples (lane-strided, ascending per lane: a strict '>' keeps the
@@ -798,6 +942,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
             }
         }
         W64_MARK();
+    #endif
     }
 #ifdef TDOA_DIAG
     stamp[13] = __builtin_amdgcn_s_memtime();
@@ -825,7 +970,7 @@ extern "C" int tdoa_diag_fetch_w64(unsigned long long *host, int n)
 namespace {
 constexpr size_t w64_lds(int U)
 {
-    return (void)U, (size_t)W64_TILES + (size_t)W64_NW * W64_TILE + W64_NW * 4;
+    return (void)U, (size_t)W64_LDS_BYTES;
 }
 }  // namespace
 
@@ -894,7 +1039,8 @@ void tdoa_p1k_w64_image(int M, int N, int K, int U, const int32_t *win, const fl
     // pair; padding tuple (127, 127, 127) scores -inf
     for (int e = 0; e < Upad; e++) {
         const uint32_t wd = e < U ? tuples[e] : 0x007F7F7Fu;
-        t[e] = ((wd & 0xFFu) << 2) | (((wd >> 8) & 0xFFu) << 12) | (((wd >> 16) & 0xFFu) << 22);
+        const int sh = W64_PAIR ? 3 : 2;  // byte offsets of f2 (paired) / f32 slots
+        t[e] = ((wd & 0xFFu) << sh) | (((wd >> 8) & 0xFFu) << (10 + sh)) | (((wd >> 16) & 0xFFu) << (20 + sh));
     }
 }
 

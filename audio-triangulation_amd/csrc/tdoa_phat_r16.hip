@@ -824,6 +824,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             wave_argmax_key(bkey, bk);
             bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
             const size_t gb = (size_t)(fr * P + p) * K;
+            // compact scratch for k_grid_bb: only lags [lo, lo + w) of the pair
+            float *wc = kernarg_out()->weighted_c;
+            const int wlo = kp.wc_lo[p], ww = kp.wc_w[p];
+            float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + kp.wc_off[p] - wlo : nullptr;
             if (oka) {
                 const int dd = ka > bk ? ka - bk : bk - ka;
                 const float wa = sa * priorl[dd];
@@ -831,6 +835,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                     out.scores_f[gb + ka] = sa;
                 if (out.weighted_f)
                     out.weighted_f[gb + ka] = wa;
+                if (wcp && ka >= wlo && ka < wlo + ww)
+                    wcp[ka] = wa;
             }
             if (okb) {
                 const int dd = kb > bk ? kb - bk : bk - kb;
@@ -839,6 +845,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                     out.scores_f[gb + kb] = sb;
                 if (out.weighted_f)
                     out.weighted_f[gb + kb] = wb;
+                if (wcp && kb >= wlo && kb < wlo + ww)
+                    wcp[kb] = wb;
             }
             if (float *pk3 = kernarg_out()->peak3) {
                 // the least-squares refinement's raw scores around the peak:
