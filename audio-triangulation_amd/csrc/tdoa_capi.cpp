@@ -1016,6 +1016,15 @@ extern "C" int tdoa_get_prior(const tdoa_ctx *c, float *scale)
 
 extern "C" const char *tdoa_last_error(void) { return g_err.c_str(); }
 
+extern "C" const char *tdoa_batch_kernel(const tdoa_ctx *ctx)
+{
+    if (!ctx)
+        return "";
+    if (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT)
+        return tdoa_gcc_phat_kernel_name(ctx->kp);
+    return tdoa_direct_fused_grid(ctx->kp) ? "k_direct_mfma" : "k_direct";
+}
+
 extern "C" int tdoa_abi_version(void) { return TDOA_ABI_VERSION; }
 
 // used by tdoa_kernels.hip launchers

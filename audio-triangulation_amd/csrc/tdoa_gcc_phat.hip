@@ -687,6 +687,19 @@ static bool use_w64(const tdoa_kparams &kp)
 }
 
 bool tdoa_phat_r16_fits(int M, int N, int S);
+bool frame16_shape(const tdoa_kparams &kp);
+
+const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp)
+{
+    if (use_w64(kp))
+        return "k_p1k_w64";
+    if (tdoa_phat1024_fits(kp))
+        return "k_p1k_lean";
+    if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
+        return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) ? (frame16_shape(kp) ? "k_frame16" : "k_spec16")
+                                                   : "k_phat_spectra";
+    return "k_gcc_phat";
+}
 int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                          float phat_eps, void *scratch, size_t scratch_bytes, void *stream);
 

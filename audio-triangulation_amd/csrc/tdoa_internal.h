@@ -241,6 +241,8 @@ void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int3
 void tdoa_p1k_w64_image(int M, int N, int K, int U, const int32_t *win, const float *prior,
                         const uint32_t *tuples, std::vector<uint8_t> &img);
 bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
+// the first kernel a GCC-PHAT batch runs for this shape (tdoa_batch_kernel)
+const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp);
 // the float grid runs k_grid_bb and can read the compact scratch (tdoa_grid.hip)
 bool tdoa_grid_bb_compact(const tdoa_kparams &kp);
 bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp);

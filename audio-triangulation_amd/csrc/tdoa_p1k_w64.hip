@@ -67,10 +67,15 @@ static_assert(IMG_FIXED % 16 == 0, "tuple table must stay 16-B aligned");
 // The image sits at the start of LDS, so every table read is a lane base plus
 // an instruction offset (< 64 KiB); the tiles follow at W64_TILES.
 constexpr int W64_UMAX = 2560;                    // padded tuple count the layout holds
-constexpr int W64_TILES = IMG_FIXED + W64_UMAX * 4;
-// + words: [16] balance, [16] pair flags, [16][4] pair exchange; then bin 512
+// LDS: [0, HDR) the small per-wave words (balance, pair flags, exchange) and
+// bin-512 slots, addressed by instruction offsets; then the image; then tiles
 constexpr int W64_WORDS = W64_NW * 6;
-constexpr int W64_LDS_BYTES = W64_TILES + W64_NW * W64_TILE + W64_WORDS * 4 + W64_NW * 16;
+constexpr int W64_B512 = 512;                     // [16 waves][2] f2
+constexpr int W64_HDR = 1024;
+static_assert(W64_WORDS * 4 <= W64_B512 && W64_B512 + W64_NW * 16 <= W64_HDR, "LDS header overflow");
+constexpr int W64_TILES = W64_HDR + IMG_FIXED + W64_UMAX * 4;
+// + words: [16] balance, [16] pair flags, [16][4] pair exchange; then bin 512
+constexpr int W64_LDS_BYTES = W64_TILES + W64_NW * W64_TILE;
 static_assert(W64_LDS_BYTES <= 160 * 1024, "k_p1k_w64 exceeds the CU's LDS");
 
 // residue column held by lane L (0..63): lane pairs (2i, 2i+1) hold partner
@@ -549,7 +554,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
     // constants that fold into the instruction offsets (the dynamic segment's
     // base is a link-time relocation, materialised by an add at every use)
     __shared__ __attribute__((aligned(16))) char smem[W64_LDS_BYTES];
-    char *img = smem;                                // table image
+    char *img = smem + W64_HDR;                      // table image
     char *tiles = smem + W64_TILES;                  // [NW][TILE]
     const float *prior = (const float *)(img + IMG_PRIOR);
     const uint32_t *tups = (const uint32_t *)(img + IMG_FIXED);
@@ -570,7 +575,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
     do {           \
     } while (0)
 #endif
-    int *prog = (int *)(tiles + W64_NW * W64_TILE);  // [SIMD group][4], after the tiles
+    int *prog = (int *)smem;  // [SIMD group][4] balance, [16] pair flags, [16][4] exchange
     if (lane == 0) {
         prog[(wave & 3) * 4 + (wave >> 2)] = 0;
         prog[W64_NW + wave] = 0;  // pair flag (read after the staging barrier)
@@ -584,7 +589,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
     W.tile = tiles + __builtin_amdgcn_readfirstlane(wave) * W64_TILE;
     W.img = img;
     W.L8 = 8 * lane;
-    W.b512 = (f2 *)(tiles + W64_NW * W64_TILE + W64_WORDS * 4) + 2 * __builtin_amdgcn_readfirstlane(wave);
+    W.b512 = (f2 *)(smem + W64_B512) + 2 * __builtin_amdgcn_readfirstlane(wave);
     auto balance = [&]() {
         if (W64_BAL >= 1)
             w64_balance(W);
@@ -776,13 +781,13 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
         // this wave's steps: u = 256 (2 j + odd), pipelined by one step
         uint32_t qa[4];
         f2 ga[4][3];
-        const int nst = Upad / 256;
+        const int nstep = Upad / 256;
 #pragma unroll
         for (int i = 0; i < 4; i++)
             qa[i] = tups[256 * odd + 64 * i + lane];
         gather(qa, ga);
-        for (int st = odd; st < nst; st += 2) {
-            const int sn = st + 2 < nst ? st + 2 : st;  // (a harmless re-read)
+        for (int st = odd; st < nstep; st += 2) {
+            const int sn = st + 2 < nstep ? st + 2 : st;  // (a harmless re-read)
             uint32_t qn[4];
 #pragma unroll
             for (int i = 0; i < 4; i++)

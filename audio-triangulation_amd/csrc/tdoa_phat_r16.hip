@@ -908,11 +908,13 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
     return 0;
 }
 
+}  // namespace
 // the fused per-frame kernel's shapes (one group of threads per mic)
 bool frame16_shape(const tdoa_kparams &kp)
 {
     return (kp.N == 4096 && (kp.M == 3 || kp.M == 4)) || (kp.N == 2048 && (kp.M == 4 || kp.M == 8));
 }
+namespace {
 
 __global__ void k_r16_gate(const int32_t *__restrict__ lags, uint8_t *__restrict__ gate, int64_t B, int P)
 {

@@ -98,6 +98,10 @@ class Localizer:
             pass
 
     # ---------------------------------------------------------- tables
+    def batch_kernel(self) -> str:
+        """Name of the kernel a batch of this context runs first (tdoa_batch_kernel)."""
+        return (load().tdoa_batch_kernel(self._ctx) or b"").decode()
+
     def window(self) -> np.ndarray:
         w = np.zeros(self.dims.N, np.int32)
         check(load().tdoa_get_window(self._ctx, w.ctypes.data_as(C.c_void_p)), "tdoa_get_window")

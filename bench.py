@@ -44,6 +44,19 @@ import torch  # noqa: E402
 from tdoa import shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CALIB_JSON = os.path.join(ROOT, "profiles", "r04_hbm_calibration.json")
+
+
+def achievable_hbm():
+    """Measured achievable HBM read rate (tools/hbm_copy.hip under rocprofv3,
+    profiles/r04_hbm_calibration.json): the denominator of frac_achievable."""
+    try:
+        c = json.load(open(CALIB_JSON))
+        return float(c["read_gbs_rocprof"]), float(c["copy_gbs_rocprof"])
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 VALU_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak
 
 # BASELINE.json configs 1-5.  batch: per GPU (weak) or global (strong).
@@ -67,10 +80,11 @@ CONFIGS = {
 }
 
 
-def dominant_kernel(config: int, engine: str) -> str:
-    """Name of the kernel(s) a launch runs (the ones `traffic` was measured on)."""
+def dominant_kernel(config: int, engine: str, first: str = "") -> str:
+    """Name of the kernel(s) a launch runs (the ones `traffic` was measured on);
+    `first` is the library's own answer (Localizer.batch_kernel)."""
     if config == 2:
-        return "k_p1k_lean" if engine == "gcc_phat" else "k_direct_mfma"
+        return first or ("k_p1k_lean" if engine == "gcc_phat" else "k_direct_mfma")
     if config in (3, 4) and engine == "gcc_phat":
         return "k_frame16 + k_grid_bb"
     return ""
@@ -236,6 +250,7 @@ def time_engine(engine, args, dev, ri, cache):
     bytes_per_loc = M * N * 2 + 4 * P + 8 + (12 if ls else 0)
     res = {
         "engine": engine,
+        "kernel": loc.batch_kernel(),
         "value": total / t["wall_max_s"],
         "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
         "kernel_ms": kern_s * 1e3,
@@ -501,10 +516,10 @@ def cpu_baseline(args, lut, window):
                       f"vga_heatmap.h algorithm, DIRECT integer xcorr), OpenMP {threads} threads"}
 
 
-def traffic_entry(args):
+def traffic_entry(args, first=""):
     """HBM bytes per launch from the committed PMC passes, used only when they
     were taken on the kernel this run dispatches."""
-    kname = dominant_kernel(args.config, args.engine)
+    kname = dominant_kernel(args.config, args.engine, first)
     if not kname or not os.path.exists(args.traffic_json):
         return None, None
     try:
@@ -545,6 +560,16 @@ def stream_traffic(args):
     return sum(per), (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / "
                       f"WRITE_SIZE passes on {' + '.join(names)} ({e.get('date', 'undated')}), "
                       "read = 2 x FETCH_SIZE; the trigger re-reads the two previous hops")
+
+
+def _achievable(achieved_gbs):
+    """frac against the measured achievable read rate beside the spec fraction."""
+    rd, cp = achievable_hbm()
+    if not rd:
+        return {"achievable": None, "frac_achievable": None}
+    return {"achievable": rd, "frac_achievable": achieved_gbs / rd,
+            "achievable_source": f"{os.path.relpath(CALIB_JSON, ROOT)}: 16-B-per-lane read sweep over 1 GiB "
+                                 f"(rocprofv3 {rd:.0f} GB/s; copy {cp:.0f} GB/s read+write)"}
 
 
 def launch_workers(args):
@@ -636,7 +661,7 @@ def main():
                             ri, cache)
     world = shard.ranks_seen()
     if ri.rank == 0:
-        traffic, tsrc = traffic_entry(args)
+        traffic, tsrc = traffic_entry(args, main_res.get("kernel", ""))
         cfg = CONFIGS[args.config]
         shape = f"{cfg['M']}-mic x {cfg['N']}-sample frames"
         B = main_res["frames_per_rank"]
@@ -673,9 +698,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": main_res["achieved_gbs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": main_res["achieved_gbs"] / HBM_PEAK_GBS,
+                         **_achievable(main_res["achieved_gbs"]),
                          "traffic": traffic,
                          "traffic_source": tsrc,
-                         "kernel": dominant_kernel(args.config, args.engine) or "all kernels of a launch",
+                         "kernel": dominant_kernel(args.config, args.engine, main_res.get("kernel", ""))
+                         or "all kernels of a launch",
                          "kernel_ms": main_res["kernel_ms"],
                          "bytes_per_loc": main_res["bytes_per_loc"]},
             # the bound that actually binds an fp32 FFT path: FP32 vector issue

@@ -212,6 +212,9 @@ int tdoa_stream_destroy(tdoa_stream *st);
 
 const char *tdoa_last_error(void);
 int tdoa_abi_version(void);
+/* Name of the kernel a tdoa_localize_batch call of this context runs first
+ * (diagnostics: profile and HBM-traffic attribution); "" if none applies. */
+const char *tdoa_batch_kernel(const tdoa_ctx *ctx);
 
 #ifdef __cplusplus
 }
