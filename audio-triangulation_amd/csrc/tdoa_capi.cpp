@@ -841,6 +841,13 @@ int tdoa_resident_blocks(const void *kernel, int threads, size_t lds)
     return r;
 }
 
+// A/B switch of the environment: set and not "0"
+static bool env_flag(const char *name)
+{
+    const char *e = getenv(name);
+    return e && *e && strcmp(e, "0") != 0;
+}
+
 static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,
                      void *stream, bool prepared)
 {
@@ -867,7 +874,7 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     // the per-frame long-frame kernel (k_frame16) can write only the lags the
     // grid reads, compacted, when k_grid_bb solves the grid (configs 3, 4)
     const bool compact = grid && !weighted && !fused_grid && phat && tdoa_gcc_phat_peak3(ctx->kp) &&
-                         tdoa_grid_bb_compact(ctx->kp) && !getenv("TDOA_NO_COMPACT");
+                         tdoa_grid_bb_compact(ctx->kp) && !env_flag("TDOA_NO_COMPACT");
     if (compact) {
         int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, (size_t)B * ctx->kp.wc_CK * sizeof(float), stream,
                       "weighted-score");

@@ -224,13 +224,16 @@ __global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out
                         if (c < nch) {
                             float *d = reinterpret_cast<float *>(Wl) + (dsc[i] & 0xFFFFu);
                             const int n = (int)(dsc[i] >> 16);
-                            d[0] = __builtin_bit_cast(float, t[i].x);
+                            // scalar copies first: __builtin_bit_cast of an
+                            // ext_vector element reads element 0 with this compiler
+                            const unsigned u0 = t[i].x, u1 = t[i].y, u2 = t[i].z, u3 = t[i].w;
+                            d[0] = __uint_as_float(u0);
                             if (n > 1)
-                                d[1] = __builtin_bit_cast(float, t[i].y);
+                                d[1] = __uint_as_float(u1);
                             if (n > 2)
-                                d[2] = __builtin_bit_cast(float, t[i].z);
+                                d[2] = __uint_as_float(u2);
                             if (n > 3)
-                                d[3] = __builtin_bit_cast(float, t[i].w);
+                                d[3] = __uint_as_float(u3);
                         }
                     }
                 }

@@ -251,10 +251,10 @@ __host__ __device__ constexpr uint32_t w64_lane_info(int L, int w)
 }
 
 #ifndef W64_PAIR
-#define W64_PAIR 1  // grid solve of two frames per gather (waves w, w ^ 1)
+#define W64_PAIR 0  // 1: grid solve of two frames per gather (waves w, w ^ 1; measured slower)
 #endif
 #ifndef W64_BAL
-#define W64_BAL 2  // issue balance: 0 none, 1 at phase boundaries, 2 also inside the transforms
+#define W64_BAL 1  // issue balance: 0 none, 1 at phase boundaries, 2 also inside the transforms
 #endif
 
 struct W64Lane {
