@@ -6,7 +6,7 @@
 //   op_sel[i]    picks the dword of source i that feeds the LOW result,
 //   op_sel_hi[i] the dword that feeds the HIGH result (default 1 = high),
 //   neg_lo / neg_hi negate source i's input to the low / high result.
-// Used by the config-2 kernel (tdoa_phat1024.hip) only.
+// Used by the GCC-PHAT kernels (tdoa_phat1024.hip, tdoa_p1k_w64.hip, tdoa_phat_r16.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -272,5 +272,36 @@ __device__ __forceinline__ void fft32p(f2 (&v)[32])
         }
     }
 }
+
+// LDS read the backend does not merge into ds_read2_b64 (a volatile
+// access; volatile reads stay in order among themselves only): two
+// ds_read_b64 take 4 LDS cycles, one ds_read2_b64 8, and ds_read2 banks by
+// (a/4) mod 32 (MI355X_MICROARCH.md LDS table)
+__device__ __forceinline__ f2 lds_rd(const f2 *p)
+{
+    typedef __attribute__((address_space(3))) f2 lds_f2;
+    return *(const volatile lds_f2 *)(const lds_f2 *)p;
+}
+
+// half exchange of two complex registers across lane bit 5 (vdst = a: lanes
+// 32-63 of a <-> lanes 0-31 of b) / lane bit 4 (odd rows of a <-> even rows of b).
+// The components go through scalar copies: __builtin_bit_cast of an
+// ext_vector element (a.y) reads element 0 with this compiler.
+template <bool X32>
+__device__ __forceinline__ void pswap(f2 &a, f2 &b)
+{
+    const float ax = a.x, ay = a.y, bx = b.x, by = b.y;
+    const unsigned uax = __float_as_uint(ax), uay = __float_as_uint(ay), ubx = __float_as_uint(bx),
+                   uby = __float_as_uint(by);
+    const auto rx = X32 ? __builtin_amdgcn_permlane32_swap(uax, ubx, false, false)
+                        : __builtin_amdgcn_permlane16_swap(uax, ubx, false, false);
+    const auto ry = X32 ? __builtin_amdgcn_permlane32_swap(uay, uby, false, false)
+                        : __builtin_amdgcn_permlane16_swap(uay, uby, false, false);
+    const unsigned r0 = rx[0], r1 = rx[1], r2 = ry[0], r3 = ry[1];
+    a = f2{__uint_as_float(r0), __uint_as_float(r2)};
+    b = f2{__uint_as_float(r1), __uint_as_float(r3)};
+}
+__device__ __forceinline__ void pswap32(f2 &a, f2 &b) { pswap<true>(a, b); }
+__device__ __forceinline__ void pswap16(f2 &a, f2 &b) { pswap<false>(a, b); }
 
 }  // namespace

@@ -688,6 +688,7 @@ static bool use_w64(const tdoa_kparams &kp)
 
 bool tdoa_phat_r16_fits(int M, int N, int S);
 bool frame16_shape(const tdoa_kparams &kp);
+const char *frame16_kernel_name(const tdoa_kparams &kp);
 
 const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp)
 {
@@ -696,7 +697,7 @@ const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp)
     if (tdoa_phat1024_fits(kp))
         return "k_p1k_lean";
     if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
-        return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) ? (frame16_shape(kp) ? "k_frame16" : "k_spec16")
+        return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) ? (frame16_shape(kp) ? frame16_kernel_name(kp) : "k_spec16")
                                                    : "k_phat_spectra";
     return "k_gcc_phat";
 }

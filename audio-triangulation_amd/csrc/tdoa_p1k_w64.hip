@@ -153,26 +153,7 @@ __device__ __forceinline__ void fft16d(f2 (&x)[16])
         x[k] = v[k];
 }
 
-// half exchange of two complex registers across lane bit 5 (vdst = a: lanes
-// 32-63 of a <-> lanes 0-31 of b) / lane bit 4 (odd rows of a <-> even rows of b).
-// The components go through scalar copies: __builtin_bit_cast of an
-// ext_vector element (a.y) reads element 0 with this compiler.
-template <bool X32>
-__device__ __forceinline__ void pswap(f2 &a, f2 &b)
-{
-    const float ax = a.x, ay = a.y, bx = b.x, by = b.y;
-    const unsigned uax = __float_as_uint(ax), uay = __float_as_uint(ay), ubx = __float_as_uint(bx),
-                   uby = __float_as_uint(by);
-    const auto rx = X32 ? __builtin_amdgcn_permlane32_swap(uax, ubx, false, false)
-                        : __builtin_amdgcn_permlane16_swap(uax, ubx, false, false);
-    const auto ry = X32 ? __builtin_amdgcn_permlane32_swap(uay, uby, false, false)
-                        : __builtin_amdgcn_permlane16_swap(uay, uby, false, false);
-    const unsigned r0 = rx[0], r1 = rx[1], r2 = ry[0], r3 = ry[1];
-    a = f2{__uint_as_float(r0), __uint_as_float(r2)};
-    b = f2{__uint_as_float(r1), __uint_as_float(r3)};
-}
-__device__ __forceinline__ void pswap32(f2 &a, f2 &b) { pswap<true>(a, b); }
-__device__ __forceinline__ void pswap16(f2 &a, f2 &b) { pswap<false>(a, b); }
+// pswap32 / pswap16: tdoa_cplx.h
 
 // Partner swap of the upper eight bins (registers 8..15) between lanes 2i and
 // 2i+1 (DPP quad_perm [1,0,3,2]) for every lane but 0 and 1; lane 0 (residue 0,

@@ -31,6 +31,8 @@
 #include <climits>
 #include <type_traits>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 // the long-frame kernels measured faster with the asm constant-twiddle
 // products (k_frame16<2048, 8>: 123.4 vs 127.4 ms per 1e6 frames)
@@ -50,6 +52,17 @@ template <int C>
 constexpr int r16_row() { return C + 32; }
 
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+// LDS reads of the fused long-frame kernels: volatile (never merged into
+// ds_read2_b64, which costs twice the LDS cycles of two ds_read_b64) unless
+// F16_VLDS=0
+#ifndef F16_VLDS
+#define F16_VLDS 1
+#endif
+#if F16_VLDS
+#define F16_LD(p) lds_rd(p)
+#else
+#define F16_LD(p) (*(p))
+#endif
 // padded offset of o, a multiple of 16: pidx(i + o) == pidx(i) + po(o) -- the
 // k_frame16 accesses are a per-thread base plus compile-time offsets (folded
 // into the ds instruction) instead of a shift and add per access
@@ -466,8 +479,12 @@ __device__ __forceinline__ void static_for(F &&f)
 
 #ifdef TDOA_DIAG
 // diagnostic build only: s_memtime per phase boundary (32 per wave: stamps
-// 0..28, [29] end of the first frame, [30] / [31] realtime start / end), per
-// wave of the first 128 workgroups
+// 0..28, [29] end of the stamped frame, [30] / [31] realtime start / end), per
+// wave of the first 128 workgroups.  The stamped frame is the workgroup's
+// frame number F16_DIAG_FRAME (default 2: steady state, not the cold start)
+#ifndef F16_DIAG_FRAME
+#define F16_DIAG_FRAME 2
+#endif
 __device__ unsigned long long g_diag_f16[1 << 16];
 #define F16_MARK()                                       \
     do {                                                 \
@@ -479,6 +496,101 @@ __device__ unsigned long long g_diag_f16[1 << 16];
     do {           \
     } while (0)
 #endif
+
+// forward transform of mic g by its group of T threads (k_spec16's front end
+// and three register passes in the group's LDS slot buf): the DC sum of the
+// group's words w, the Q15 window, radix R1 / 16 / 16 Stockham passes; Z[j + T q]
+// ends in buf at pidx(j + T q), after a closing barrier
+template <int C>
+__device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, f2 *buf, int *red,
+                                                const f2 *tt, int tid, int g, int j, int pj, int log2N)
+{
+    constexpr int T = C / 16, R1 = C / 256;
+    uint32_t wn[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        wn[s] = win[j + T * s];
+    int sum = 0;
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_r16, w[s]), v2s_r16{1, 1}, sum, false);
+    sum = group_sum_dpp(sum, 64);  // DPP moves to lane 63 (no LDS round trips)
+    if ((tid & 63) == 63)
+        red[tid >> 6] = sum;
+    __syncthreads();
+    sum = 0;
+#pragma unroll
+    for (int wv = 0; wv < T / 64; wv++)
+        sum += red[g * (T / 64) + wv];
+    const uint32_t off = (uint32_t)(sum >> log2N) & 0xFFu;
+    const uint32_t off2 = off | (off << 16);
+    f2 v[16];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const uint32_t d = (w[s] | 0x01000100u) - off2;
+        const float s0 = (float)(int8_t)(d & 0xFFu), s1 = (float)(int8_t)((d >> 16) & 0xFFu);
+        const float w0 = (float)(int16_t)(wn[s] & 0xFFFFu) * (1.0f / 128.0f);
+        const float w1 = (float)(int16_t)(wn[s] >> 16) * (1.0f / 128.0f);
+        v[s] = f2{floorf(s0 * w0), floorf(s1 * w1)};
+    }
+    if constexpr (R1 == 16) {
+#pragma unroll
+        for (int s = 8; s < 16; s++)
+            v[s] = f2{0.0f, 0.0f};
+        dftp<16, false, true>(v);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            buf[17 * j + r] = v[brev<16>(r)];  // pidx(16 j + r)
+    } else {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            f2 u[8];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                u[r] = v[2 * r + h];
+#pragma unroll
+            for (int r = 4; r < 8; r++)
+                u[r] = f2{0.0f, 0.0f};
+            dftp<8, false, true>(u);
+            // pidx(8 (j + 128 h) + r) = 8 j + (j >> 1) + 1088 h + r (r < 8)
+#pragma unroll
+            for (int r = 0; r < 8; r++)
+                buf[8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
+        }
+    }
+    __syncthreads();
+    {
+        const int k = j % R1;
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = F16_LD(buf + pj + po(T * r));
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
+        dftp<16, false, false>(v);
+        __syncthreads();
+        // o mod 16 = k < R1: pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16
+        const int o = pidx((j / R1) * 16 * R1 + k);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            buf[o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
+    }
+    __syncthreads();
+    {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            v[r] = F16_LD(buf + pj + po(T * r));
+#pragma unroll
+        for (int r = 1; r < 16; r++)
+            v[r] = c_mul(v[r], c_mul(F16_LD(tt + 256 + 16 * r + (j & 15)), F16_LD(tt + 512 + 16 * r + (j >> 4))));  // twC
+        dftp<16, false, false>(v);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
+            buf[pj + po(T * q)] = v[brev<16>(q)];
+    }
+    __syncthreads();
+}
 
 // LDS bytes of k_frame16
 template <int C>
@@ -554,7 +666,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #ifdef TDOA_DIAG
     unsigned long long stamp[32] = {};
     int nst = 0;
-    stamp[30] = __builtin_amdgcn_s_memrealtime();
+    const int64_t diag_fr = blockIdx.x + (B >= (int64_t)(F16_DIAG_FRAME + 1) * gridDim.x ? F16_DIAG_FRAME : 0) *
+                                             (int64_t)gridDim.x;
+#else
+    constexpr int64_t diag_fr = -1;
 #endif
     // persistent over frames (one workgroup per CU): the next frame's words are
     // requested when the pair rounds start, so their HBM latency hides behind
@@ -572,97 +687,16 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // thread indices the compiler cannot prove loop-invariant: the passes'
     // twiddle reads stay in the body instead of being hoisted (and spilled)
     const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T, pj = pidx(j);
-    if (fr == blockIdx.x)
+    if (fr == diag_fr) {
+#ifdef TDOA_DIAG
+        stamp[30] = __builtin_amdgcn_s_memrealtime();
+#endif
         F16_MARK();
+    }
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
-    {
-        uint32_t wn[8];
-#pragma unroll
-        for (int s = 0; s < 8; s++)
-            wn[s] = win[j + T * s];
-        int sum = 0;
-#pragma unroll
-        for (int s = 0; s < 8; s++)
-            sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s_r16, w[s]), v2s_r16{1, 1}, sum, false);
-        sum = group_sum_dpp(sum, 64);  // DPP moves to lane 63 (no LDS round trips)
-        if ((tid & 63) == 63)
-            red[tid >> 6] = sum;
-        __syncthreads();
-        sum = 0;
-#pragma unroll
-        for (int wv = 0; wv < T / 64; wv++)
-            sum += red[g * (T / 64) + wv];
-        const uint32_t off = (uint32_t)(sum >> kp.log2N) & 0xFFu;
-        const uint32_t off2 = off | (off << 16);
-        f2 v[16];
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            const uint32_t d = (w[s] | 0x01000100u) - off2;
-            const float s0 = (float)(int8_t)(d & 0xFFu), s1 = (float)(int8_t)((d >> 16) & 0xFFu);
-            const float w0 = (float)(int16_t)(wn[s] & 0xFFFFu) * (1.0f / 128.0f);
-            const float w1 = (float)(int16_t)(wn[s] >> 16) * (1.0f / 128.0f);
-            v[s] = f2{floorf(s0 * w0), floorf(s1 * w1)};
-        }
-        if constexpr (R1 == 16) {
-#pragma unroll
-            for (int s = 8; s < 16; s++)
-                v[s] = f2{0.0f, 0.0f};
-            dftp<16, false, true>(v);
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                buf[17 * j + r] = v[brev<16>(r)];  // pidx(16 j + r)
-        } else {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                f2 u[8];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-                    u[r] = v[2 * r + h];
-#pragma unroll
-                for (int r = 4; r < 8; r++)
-                    u[r] = f2{0.0f, 0.0f};
-                dftp<8, false, true>(u);
-                // pidx(8 (j + 128 h) + r) = 8 j + (j >> 1) + 1088 h + r (r < 8)
-#pragma unroll
-                for (int r = 0; r < 8; r++)
-                    buf[8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
-            }
-        }
-        __syncthreads();
-        {
-            const int k = j % R1;
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                v[r] = buf[pj + po(T * r)];
-#pragma unroll
-            for (int r = 1; r < 16; r++)
-                v[r] = c_mul(v[r], tw16h(tt, r, k));
-            dftp<16, false, false>(v);
-            __syncthreads();
-            // o mod 16 = k < R1: pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16
-            const int o = pidx((j / R1) * 16 * R1 + k);
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                buf[o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
-        }
-        __syncthreads();
-        {
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                v[r] = buf[pj + po(T * r)];
-#pragma unroll
-            for (int r = 1; r < 16; r++)
-                v[r] = c_mul(v[r], twC(tt, r, j));
-            dftp<16, false, false>(v);
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
-                buf[pj + po(T * q)] = v[brev<16>(q)];
-        }
-        __syncthreads();
-    }
-    if (fr == blockIdx.x)
+    frame16_forward<C>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N);
+    if (fr == diag_fr)
         F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
     // X[b] = (Z[b] + Z*[C-b]) - i W_2C^b (Z[b] - Z*[C-b]), X[C-b] = conj(e + i W od)
@@ -684,7 +718,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
         for (int m = 0; m < M; m++) {
             const f2 *zb = bufs + m * BUF;
-            const f2 z = zb[pb], zp = zb[pp];
+            const f2 z = F16_LD(zb + pb), zp = F16_LD(zb + pp);
             const f2 e = c_addconj(z, zp);
             const f2 od = c_mul(c_subconj(z, zp), wb);
             Ub[m][s] = c_unit(c_add_mi(e, od), e2);
@@ -696,7 +730,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
     }
     __syncthreads();  // slots consumed: they become the pairs' buffers
-    if (fr == blockIdx.x)
+    if (fr == diag_fr)
         F16_MARK();  // unit spectra in registers
     {
         const int64_t fn = fr + gridDim.x;
@@ -741,7 +775,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             }
         });
         __syncthreads();
-        if (fr == blockIdx.x)
+        if (fr == diag_fr)
             F16_MARK();  // the round's Y buffers written
         const int p = p0 + g;
         const bool pair_on = p < P;
@@ -753,7 +787,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on) {
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                v[r] = buf[pjl + po(T * r)];
+                v[r] = F16_LD(buf + pjl + po(T * r));
             dftp<16, true, false>(v);
         }
         __syncthreads();
@@ -769,12 +803,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
-            f2 l0 = buf[pjl + po(T * r)], l1 = buf[pjl + po(T * (r + 4))];
-            const f2 h0 = c_mulconj(buf[pjl + po(T * (r + 8))], tw256(tt, r + 8, k));
-            const f2 h1 = c_mulconj(buf[pjl + po(T * (r + 12))], tw256(tt, r + 12, k));
+            f2 l0 = F16_LD(buf + pjl + po(T * r)), l1 = F16_LD(buf + pjl + po(T * (r + 4)));
+            const f2 h0 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 8))), F16_LD(tt + 16 * (r + 8) + k));
+            const f2 h1 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 12))), F16_LD(tt + 16 * (r + 12) + k));
             if (r)
-                l0 = c_mulconj(l0, tw256(tt, r, k));
-            l1 = c_mulconj(l1, tw256(tt, r + 4, k));
+                l0 = c_mulconj(l0, F16_LD(tt + 16 * r + k));  // tw256
+            l1 = c_mulconj(l1, F16_LD(tt + 16 * (r + 4) + k));
             const f2 a0 = l0 + h0, a1 = l1 + h1;
             const f2 d0 = dif_tw<true>(l0, h0, 2 * r), d1 = dif_tw<true>(l1, h1, 2 * (r + 4));
             x0 = x0 + (a0 + a1);
@@ -801,11 +835,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
             // the output index C - m; tw3 holds each lane's factors (conjugated for l < 32)
             const int pl = pidx(l);
-            f2 y = buf[pl];
+            f2 y = F16_LD(buf + pl);
 #pragma unroll
             for (int r = 1; r < R1; r++) {
-                const f2 u = buf[pl + 68 * r];
-                y = y + c_mul(u, tw3[64 * r + l]);
+                const f2 u = F16_LD(buf + pl + 68 * r);
+                y = y + c_mul(u, F16_LD(tw3 + 64 * r + l));
             }
             const int n = l < 32 ? l : -mm;
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
@@ -863,7 +897,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
-        if (fr == blockIdx.x)
+        if (fr == diag_fr)
             F16_MARK();
     });
     if (tid == 0 && out.gate) {
@@ -873,7 +907,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
     }
 #ifdef TDOA_DIAG
-    if (fr == blockIdx.x) {
+    if (fr == diag_fr) {
         stamp[31] = __builtin_amdgcn_s_memrealtime();
         stamp[29] = __builtin_amdgcn_s_memtime();
     }
@@ -908,11 +942,404 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
     return 0;
 }
 
+
+// ------------------------------------------------ fused, one wave per pair
+// k_frame16w<2048, 8> (BASELINE config 4).  k_frame16's forward transforms,
+// then the split writes the unit spectra U_m[0..C] back into the mics' LDS
+// slots, and every wave runs whole pairs from there on its own: no workgroup
+// barrier between the spectra and the frame's end (k_frame16 spends five per
+// round of 8 pairs, and writes every pair's inverse input and first pass
+// through LDS).  For pair (i, j), lane l of the wave:
+//   * Y[b], b = l + 64 q (q < 32): k_pair16's pre-twiddle from U_i, U_j at b
+//     and C - b, R = conj(U_i) U_j, with conj(W_2C^b) = conj(W_2C^l) conj(W_64^q)
+//     (a lane constant, then a compile-time one);
+//   * A_l[k] = sum_q Y[l + 64 q] W_32^{-q k}: a register DFT-32 (fft32d);
+//   * y[n] = sum_l W_C^{-l n} A_l[n mod 32], needed for n in [-32, 32) only:
+//     y[k] = sum_l B_l[k] and y[k - 32] = sum_l W_64^l B_l[k], B_l[k] =
+//     W_C^{-l k} A_l[k] (LDS table) -- a reduce-scatter over the wave:
+//     v_permlane32_swap (lanes 0-31 keep the y[k] sums, 32-63 the y[k - 32]
+//     ones), v_permlane16_swap (k bit 4), then DPP row_ror:8, row_half_mirror,
+//     quad_perm [1,0,3,2] and [2,3,0,1] (k bits 3, 2, 0, 1), after which lane l
+//     holds y[n] with n = l (l < 32) or l - 64: k_frame16's pass-3 lag layout;
+//   * the first argmax, the lag prior and the outputs as in k_frame16.
+// The 28 pairs go to waves w and w + 16: seven per SIMD.
+template <int C>
+struct f16w_lds {
+    static constexpr int G = 16384 / C;
+    static constexpr int SLOT = C + C / 16 + 2;  // pidx(0..C): U[C] sits at pidx(C) = C + C / 16
+    static constexpr size_t TBL = (size_t)G * SLOT * sizeof(f2);    // [31][64] W_C^{-l k}, k = 1..31
+    static constexpr size_t TT = TBL + 31 * 64 * sizeof(f2);         // [3][16][16] kp.r16_tw
+    static constexpr size_t PRIOR = TT + 3 * 16 * 16 * sizeof(f2);   // [128] the lag prior
+    static constexpr size_t RED = PRIOR + 128 * sizeof(float);       // [16] DC partial sums
+    static constexpr size_t LAG = RED + 16 * sizeof(int);            // [TDOA_MAX_PAIRS] lags
+    static constexpr size_t BYTES = LAG + TDOA_MAX_PAIRS * sizeof(int);
+};
+static_assert(f16w_lds<2048>::BYTES <= 160 * 1024, "k_frame16w LDS");
+
+// cos(2 pi q / 64), q = 0..16
+__device__ constexpr double COS64D[17] = {
+    1.0, 0.99518472667219693, 0.98078528040323043, 0.95694033573220882, 0.92387953251128674,
+    0.88192126434835505, 0.83146961230254524, 0.77301045336273699, 0.70710678118654757,
+    0.63439328416364549, 0.55557023301960229, 0.47139673682599781, 0.38268343236508984,
+    0.29028467725446233, 0.19509032201612833, 0.09801714032956077, 0.0};
+// conj(W_64^q) = e^{+2 pi i q / 64}, q < 32 (q = 0, 16: no product)
+__device__ constexpr f2 w64conj(int q)
+{
+    return q <= 16 ? f2{(float)COS64D[q], (float)COS64D[16 - q]}
+                   : f2{(float)-COS64D[32 - q], (float)COS64D[q - 16]};
+}
+
+// one step of the reduce-scatter over DPP partners: lanes with lane bit BIT
+// clear keep the sum of the registers' lo values, the others of hi
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ f2 rs_dpp(f2 lo, f2 hi, bool up)
+{
+    const float kx = up ? hi.x : lo.x, ky = up ? hi.y : lo.y;
+    const float sx = up ? lo.x : hi.x, sy = up ? lo.y : hi.y;
+    return f2{kx + dpp_f<CTRL>(sx), ky + dpp_f<CTRL>(sy)};
+}
+constexpr int DPP_QP_1032 = 0xB1;  // quad_perm [1,0,3,2]: lane bit 0 partner
+constexpr int DPP_QP_2301 = 0x4E;  // quad_perm [2,3,0,1]: lane bit 1 partner
+constexpr int DPP_ROW_HMIRROR = 0x141;  // i <-> 7 - i in each half row
+constexpr int DPP_ROW_ROR8 = 0x128;     // i <-> i ^ 8 in each row
+
+#ifndef F16W_PREFETCH_EARLY
+#define F16W_PREFETCH_EARLY 1  // the next frame's words requested before the pairs
+#endif
+#ifndef F16W_DIF
+#define F16W_DIF 0  // 1: the in-place DIF DFT-32 (fft32p) instead of the FMA DIT one
+#endif
+#ifndef F16W_QB
+#define F16W_QB 8  // bins (q) between scheduling barriers
+#endif
+#ifndef F16W_KB
+#define F16W_KB 2  // DFT outputs (k) between scheduling barriers
+#endif
+// the pruned inverse of pair (Ui, Uj) by one wave: lane l returns y[n],
+// n = l (l < 32) or l - 64, unscaled (x 2C)
+template <int C>
+__device__ __forceinline__ f2 frame16w_inverse(const f2 *Ui, const f2 *Uj, const f2 *tbl, f2 w2l, f2 oml, int lane)
+{
+    static_assert(C == 2048, "32 bins per lane");
+    constexpr int PQ = po(64);  // pidx step of one q (64 bins)
+    const int ob = lane + (lane >> 4);                        // pidx(l)
+    const int pbase = PQ - lane - ((lane + 15) >> 4);         // pidx(C - l - 64 q) = pbase + PQ (31 - q)
+    f2 y[32];
+#pragma unroll
+    for (int q = 0; q < 32; q++) {
+        const f2 Rk = c_conjmul(F16_LD(Ui + ob + PQ * q), F16_LD(Uj + ob + PQ * q));  // R[b]
+        const f2 Rq = c_conjmul(F16_LD(Ui + pbase + PQ * (31 - q)), F16_LD(Uj + pbase + PQ * (31 - q)));  // R[C-b]
+        const f2 ss = c_addconj(Rk, Rq);
+        const f2 dd = c_mulconj(c_subconj(Rk, Rq), w2l);
+        if (q == 0)
+            y[q] = c_add_i(ss, dd);
+        else if (q == 16)  // conj(W_64^16) = i: ss + i (i dd)
+            y[q] = ss - dd;
+        else
+            y[q] = c_add_i(ss, c_mul_s(dd, w64conj(q)));
+        if ((q & (F16W_QB - 1)) == F16W_QB - 1)  // bounded read-ahead (the reads all hoisted spill)
+            __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#if F16W_DIF
+    fft32p<true, false>(y);  // A_l[k] in y[brev5(k)]
+#define F16W_A(k) y[brev5(k)]
+#else
+    fft32d<true, false>(y);
+#define F16W_A(k) y[k]
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    // B = W_C^{-l k} A, C = W_64^l B; permlane32: lanes 0-31 (B_l, B_{l+32}),
+    // lanes 32-63 (C_l, C_{l+32})
+    f2 z[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        f2 b = k == 0 ? F16W_A(0) : c_mul(F16W_A(k), F16_LD(tbl + (k - 1) * 64 + lane));
+        f2 c = c_mul(b, oml);
+        pswap32(b, c);
+        z[k] = b + c;
+        asm volatile("" ::"v"(z[k]));  // the sum here: not sunk to stage 2 (both halves live until then)
+        if ((k & (F16W_KB - 1)) == F16W_KB - 1)
+            __builtin_amdgcn_sched_barrier(0);
+    }
+#undef F16W_A
+    // permlane16: even rows keep k, odd rows k + 16
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        f2 a = z[k], b = z[k + 16];
+        pswap16(a, b);
+        y[k] = a + b;
+    }
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        y[k] = rs_dpp<DPP_ROW_ROR8>(y[k], y[k + 8], b3);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        y[k] = rs_dpp<DPP_ROW_HMIRROR>(y[k], y[k + 4], b2);
+    y[0] = rs_dpp<DPP_QP_1032>(y[0], y[1], b0);
+    y[1] = rs_dpp<DPP_QP_1032>(y[2], y[3], b0);
+    return rs_dpp<DPP_QP_2301>(y[0], y[1], b1);
+}
+
+#ifdef TDOA_DIAG
+#define F16W_MARK()                                      \
+    do {                                                 \
+        if (nst < 29)                                    \
+            stamp[nst++] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define F16W_MARK() \
+    do {            \
+    } while (0)
+#endif
+
+// (kp, out) must stay the first two parameters: kernarg_out() reads `out`
+// at its kernarg offset
+template <int C, int M>
+__global__ void __launch_bounds__(1024, 1) k_frame16w(tdoa_kparams kp, tdoa_kout out,
+                                                      const int16_t *__restrict__ frames, int64_t B, float e2)
+{
+    using L = f16w_lds<C>;
+    constexpr int T = C / 16, G = L::G, SLOT = L::SLOT;
+    static_assert(M == G, "one forward group per mic");
+    constexpr int P = M * (M - 1) / 2;
+    static_assert(P <= 32 && P > 16, "two pair slots per wave");
+    __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
+    f2 *bufs = (f2 *)smem;
+    f2 *tbl = (f2 *)(smem + L::TBL);
+    f2 *ttl = (f2 *)(smem + L::TT);
+    float *priorl = (float *)(smem + L::PRIOR);
+    int *red = (int *)(smem + L::RED);
+    int *lagl = (int *)(smem + L::LAG);
+    const int g = (int)threadIdx.x / T;
+    const int K = kp.K, S = kp.S;
+    f2 *buf = bufs + g * SLOT;
+    const uint32_t *win = reinterpret_cast<const uint32_t *>(kp.window);
+    const f2 *tw = reinterpret_cast<const f2 *>(kp.tw);
+    const f2 *tw2 = reinterpret_cast<const f2 *>(kp.tw2);
+    if (threadIdx.x < 3 * 16 * 16)
+        ttl[threadIdx.x] = reinterpret_cast<const f2 *>(kp.r16_tw)[threadIdx.x];
+    if (threadIdx.x < (unsigned)kp.K)
+        priorl[threadIdx.x] = kp.prior[threadIdx.x];
+    for (int e = threadIdx.x; e < 31 * 64; e += 1024) {  // W_C^{-l k} = conj(kp.tw[l k])
+        const int k = (e >> 6) + 1, l = e & 63;
+        const f2 t = tw[l * k];
+        tbl[e] = f2{t.x, -t.y};
+    }
+    const int lane = (int)threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    // the wave's two pairs' table entries, read once here: a byte of kp
+    // indexed per pair is a VMEM load, and its vmcnt wait inside the frame
+    // loop would also wait for the next frame's words prefetched before the pairs
+    auto rfl = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+    const int q1 = wv + 16 < P ? wv + 16 : wv;
+    const int mi0 = rfl(kp.pair_i[wv]), mj0 = rfl(kp.pair_j[wv]);
+    const int mi1 = rfl(kp.pair_i[q1]), mj1 = rfl(kp.pair_j[q1]);
+    const int lo0 = rfl(kp.wc_lo[wv]), w0 = rfl(kp.wc_w[wv]), of0 = rfl(kp.wc_off[wv]);
+    const int lo1 = rfl(kp.wc_lo[q1]), w1 = rfl(kp.wc_w[q1]), of1 = rfl(kp.wc_off[q1]);
+    const f2 w2l = tw2[lane];       // W_2C^l: the pre-twiddle's lane factor
+    const f2 oml = tw[32 * lane];   // W_64^l = W_C^{32 l}
+    const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
+#ifdef TDOA_DIAG
+    unsigned long long stamp[32] = {};
+    int nst = 0;
+    const int64_t diag_fr = blockIdx.x + (B >= (int64_t)(F16_DIAG_FRAME + 1) * gridDim.x ? F16_DIAG_FRAME : 0) *
+                                             (int64_t)gridDim.x;
+#else
+    constexpr int64_t diag_fr = -1;
+#endif
+    uint32_t w[8];
+    auto fetch = [&](int64_t f) {
+        const uint32_t *x = reinterpret_cast<const uint32_t *>(frames + (f * M + g) * (int64_t)C) +
+                            ((int)threadIdx.x - g * T);
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            w[s] = __builtin_nontemporal_load(x + T * s);
+    };
+    fetch(blockIdx.x);
+    for (int64_t fr = blockIdx.x; fr < B; fr += gridDim.x) {
+        const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T, pj = pidx(j);
+        if (fr == diag_fr) {
+#ifdef TDOA_DIAG
+            stamp[30] = __builtin_amdgcn_s_memrealtime();
+#endif
+            F16W_MARK();
+        }
+        frame16_forward<C>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N);
+        if (fr == diag_fr)
+            F16W_MARK();  // forward transforms done
+        // ---- 2. split + unit normalisation in place: thread b writes U_m[b]
+        // and U_m[C - b] over the Z slots it read (b = 0: U_m[0], U_m[C])
+        {
+            const int b = tid;
+            const f2 wb = tw2[b];
+            const int pb = pidx(b), pr = pidx((C - b) & (C - 1)), pw = pidx(C - b);
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                f2 *zb = bufs + m * SLOT;
+                const f2 z = F16_LD(zb + pb), zp = F16_LD(zb + pr);
+                const f2 e = c_addconj(z, zp);
+                const f2 od = c_mul(c_subconj(z, zp), wb);
+                zb[pb] = c_unit(c_add_mi(e, od), e2);
+                zb[pw] = c_unit(c_conj_add_i(e, od), e2);
+            }
+            if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
+                f2 *zh = bufs + tid * SLOT + pidx(C / 2);
+                const f2 v = *zh;
+                *zh = c_unit(f2{2.0f * v.x, -2.0f * v.y}, e2);
+            }
+        }
+        __syncthreads();
+        if (fr == diag_fr)
+            F16W_MARK();  // unit spectra in the slots
+#if F16W_PREFETCH_EARLY
+        {
+            const int64_t fn = fr + gridDim.x;
+            fetch(fn < B ? fn : fr);  // the next frame's words (or a harmless re-read)
+        }
+#endif
+        // ---- 3. pairs wv and wv + 16 of this wave, no barriers
+        const float invL = 1.0f / (float)(2 * C);
+#pragma unroll 1
+        for (int h = 0; h < 2; h++) {
+            const int p = wv + 16 * h;
+            if (p >= P)
+                break;
+            const f2 *Ui = bufs + (h ? mi1 : mi0) * SLOT, *Uj = bufs + (h ? mj1 : mj0) * SLOT;
+            // the lane index re-derived per pair: the lag / address arithmetic
+            // below stays here instead of being hoisted (and spilled) above the frames
+            const int ln = opaque_idx((int)threadIdx.x) & 63;
+            const f2 yv = frame16w_inverse<C>(Ui, Uj, tbl, w2l, oml, ln);
+            const int n = ln < 32 ? ln : ln - 64;
+            const int ka = 2 * n + S, kb = 2 * n + 1 + S;
+            const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
+            const float sa = yv.x * invL, sb = yv.y * invL;
+            // first maximum (the lowest lag wins ties), by keys to every lane
+            int bkey = INT_MIN, bk = INT_MAX;
+            if (oka) {
+                bkey = fkey(sa);
+                bk = ka;
+            }
+            if (okb && fkey(sb) > bkey) {
+                bkey = fkey(sb);
+                bk = kb;
+            }
+            wave_argmax_key(bkey, bk);
+            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
+            const size_t gb = (size_t)(fr * P + p) * K;
+            float *wc = kernarg_out()->weighted_c;
+            const int wlo = h ? lo1 : lo0, ww = h ? w1 : w0;
+            float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + (h ? of1 : of0) - wlo : nullptr;
+            if (oka) {
+                const int dd = ka > bk ? ka - bk : bk - ka;
+                const float wa = sa * priorl[dd];
+                if (out.scores_f)
+                    out.scores_f[gb + ka] = sa;
+                if (out.weighted_f)
+                    out.weighted_f[gb + ka] = wa;
+                if (wcp && ka >= wlo && ka < wlo + ww)
+                    wcp[ka] = wa;
+            }
+            if (okb) {
+                const int dd = kb > bk ? kb - bk : bk - kb;
+                const float wb = sb * priorl[dd];
+                if (out.scores_f)
+                    out.scores_f[gb + kb] = sb;
+                if (out.weighted_f)
+                    out.weighted_f[gb + kb] = wb;
+                if (wcp && kb >= wlo && kb < wlo + ww)
+                    wcp[kb] = wb;
+            }
+            if (float *pk3 = kernarg_out()->peak3) {
+                float *dst = pk3 + (size_t)(fr * P + p) * 3 + 1 - bk;
+                if (oka && ka >= bk - 1 && ka <= bk + 1)
+                    dst[ka] = sa;
+                if (okb && kb >= bk - 1 && kb <= bk + 1)
+                    dst[kb] = sb;
+            }
+            if (ln == 0) {
+                out.lags[fr * P + p] = bk - S;
+                lagl[p] = bk - S;
+            }
+            if (fr == diag_fr)
+                F16W_MARK();  // a pair done
+        }
+#if !F16W_PREFETCH_EARLY
+        {
+            const int64_t fn = fr + gridDim.x;
+            fetch(fn < B ? fn : fr);
+        }
+#endif
+        __syncthreads();  // the slots are rewritten by the next frame
+        if (tid == 0 && out.gate) {
+            int tot = 0;
+            for (int q = 0; q < P; q++)
+                tot += lagl[q] * lagl[q];
+            out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+        }
+#ifdef TDOA_DIAG
+        if (fr == diag_fr) {
+            stamp[31] = __builtin_amdgcn_s_memrealtime();
+            stamp[29] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+    }
+#ifdef TDOA_DIAG
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 128)
+        for (int i = 0; i < 32; i++)
+            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + i] = stamp[i];
+#endif
+}
+#undef F16W_MARK
+
+template <int C, int M>
+int launch_frame16w(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B, float e2,
+                    hipStream_t st)
+{
+    if (B <= 0)
+        return 0;
+    const int res = tdoa_resident_blocks((const void *)k_frame16w<C, M>, 1024, 0);
+    if (res < 1)
+        return tdoa_set_error(-2, "k_frame16w: no resident workgroup (LDS / registers)");
+    const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
+    hipLaunchKernelGGL((k_frame16w<C, M>), dim3((unsigned)grid), dim3(1024), 0, st, kp, out, frames, B, e2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "k_frame16w launch: %s", hipGetErrorString(e));
+        return tdoa_set_error(-2, msg);
+    }
+    return 0;
+}
+
+// k_frame16w (one wave per pair) or k_frame16 (a group of waves per pair) for
+// config 4's shape: TDOA_F16=w | grp, default grp (measured: 106.2 vs 103.2
+// ms per config-4 step, both with volatile LDS reads)
+bool frame16w_pick()
+{
+    static const int pick = [] {
+        const char *e = getenv("TDOA_F16");
+        return e && !strcmp(e, "w") ? 1 : 0;
+    }();
+    return pick == 1;
+}
+
 }  // namespace
 // the fused per-frame kernel's shapes (one group of threads per mic)
 bool frame16_shape(const tdoa_kparams &kp)
 {
     return (kp.N == 4096 && (kp.M == 3 || kp.M == 4)) || (kp.N == 2048 && (kp.M == 4 || kp.M == 8));
+}
+// the name of the fused kernel a frame16_shape launch runs
+const char *frame16_kernel_name(const tdoa_kparams &kp)
+{
+    return kp.N == 2048 && kp.M == 8 && frame16w_pick() ? "k_frame16w" : "k_frame16";
 }
 namespace {
 
@@ -996,7 +1423,8 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (kp.N == 4096 && kp.M == 3)
         return launch_frame16<4096, 3>(kp, out, frames, B, e2, st);
     if (kp.N == 2048 && kp.M == 8)
-        return launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
+        return frame16w_pick() ? launch_frame16w<2048, 8>(kp, out, frames, B, e2, st)
+                               : launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
     if (kp.N == 2048 && kp.M == 4)
         return launch_frame16<2048, 4>(kp, out, frames, B, e2, st);
     return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)

@@ -36,7 +36,24 @@ st = st[st[:, 0] > 0]
 G = 16384 // N
 P = M * (M - 1) // 2
 R = (P + G - 1) // G
-names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} inv"] for r in range(R)], [])
+wave_kernel = cfg == 4 and os.environ.get("TDOA_F16", "w") != "grp"  # k_frame16w
+if wave_kernel:
+    # k_frame16w: start, forward, split, then one stamp per pair of the wave
+    # (waves 0-11 run two pairs, 12-15 one: their stamp 4 stays 0)
+    names = ["start", "forward", "split", "pair 1"]
+    w = np.arange(len(st)) % 16
+    two = st[w < P - 16]
+    d = two[:, 4] - two[:, 3]
+    print("k_frame16w second pair (waves with two): p10 / p50 / p90 %.0f %.0f %.0f" %
+          (np.percentile(d, 10), np.median(d), np.percentile(d, 90)))
+    print("per wave: median cycles after the split barrier to the end of pair 1 / pair 2")
+    for wi in range(16):
+        sw = st[w == wi]
+        e1 = np.median(sw[:, 3] - sw[:, 2])
+        e2 = np.median(sw[:, 4] - sw[:, 2]) if wi < P - 16 else float("nan")
+        print(f"  wave {wi:2d}: {e1:8.0f} {e2:8.0f}")
+else:
+    names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} inv"] for r in range(R)], [])
 n = len(names)
 print(f"config {cfg}: M={M} N={N} P={P} G={G} rounds={R}, waves {len(st)}")
 life = st[:, 29] - st[:, 0]
@@ -46,5 +63,5 @@ print("phase durations (cycles): p10 / p50 / p90")
 for i in range(1, n):
     d = st[:, i] - st[:, i - 1]
     print(f"  {names[i]:9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
-d = st[:, 29] - st[:, n - 1]
+d = st[:, 29] - st[:, n - 1] if not wave_kernel else st[:, 29] - np.where(st[:, 4] > 0, st[:, 4], st[:, 3])
 print(f"  {'tail':9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")

@@ -15,6 +15,7 @@
 #   ablib[:L1,L2,..]      bench config 2 once per library tdoa/<L>.so (TDOA_LIB)
 #   testlib:L[:FILES]     pytest -m gpu against tdoa/<L>.so
 #   diagw64               phase stamps of k_p1k_w64 (needs the diag library)
+#   diagf16[:CFG]         phase stamps of k_frame16 (config 3 or 4, diag library)
 #   calib                 tools/hbm_copy (achievable HBM), plain and under rocprofv3
 #   smoke                 __graft_entry__.smoke()
 #
@@ -136,6 +137,13 @@ for step in "$@"; do
         # phase stamps of k_p1k_w64 (libtdoa_diag.so, make -C audio-triangulation_amd diag)
         timeout -k 10 120 python tools/diag_w64.py > "$OUT/diag_w64.txt" 2>&1 || { tail -5 "$OUT/diag_w64.txt"; exit 32; }
         cat "$OUT/diag_w64.txt"
+        ;;
+    diagf16)
+        # phase stamps of k_frame16 (needs the diag library): diagf16:CFG
+        c=$(field "$step" 2 4)
+        timeout -k 10 120 python tools/diag_frame16.py $c 8192 > "$OUT/diag_f16_c$c.txt" 2>&1 \
+            || { tail -5 "$OUT/diag_f16_c$c.txt"; exit 33; }
+        cat "$OUT/diag_f16_c$c.txt"
         ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
