@@ -157,9 +157,18 @@ __device__ __forceinline__ int hsum32(int s, int hw)
     return hw ? s1 : s0;
 }
 
+// LDS reads: volatile ds_read_b64 unless P1K_VLDS=0 (the backend otherwise
+// merges neighbours into ds_read2_b64, twice the LDS cycles of two b64 reads)
+#ifndef P1K_VLDS
+#define P1K_VLDS 1
+#endif
 __device__ __forceinline__ f2 lds_f2(const char *base, int off)
 {
+#if P1K_VLDS
+    return lds_rd(reinterpret_cast<const f2 *>(base + off));
+#else
     return *reinterpret_cast<const f2 *>(base + off);
+#endif
 }
 __device__ __forceinline__ void sts_f2(char *base, int off, f2 v)
 {

@@ -966,7 +966,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 template <int C>
 struct f16w_lds {
     static constexpr int G = 16384 / C;
-    static constexpr int SLOT = C + C / 16 + 2;  // pidx(0..C): U[C] sits at pidx(C) = C + C / 16
+    static constexpr int SLOT = C + C / 16 + 2;  // Z at pidx(0..C-1), then U at 0..C
     static constexpr size_t TBL = (size_t)G * SLOT * sizeof(f2);    // [31][64] W_C^{-l k}, k = 1..31
     static constexpr size_t TT = TBL + 31 * 64 * sizeof(f2);         // [3][16][16] kp.r16_tw
     static constexpr size_t PRIOR = TT + 3 * 16 * 16 * sizeof(f2);   // [128] the lag prior
@@ -1026,9 +1026,9 @@ template <int C>
 __device__ __forceinline__ f2 frame16w_inverse(const f2 *Ui, const f2 *Uj, const f2 *tbl, f2 w2l, f2 oml, int lane)
 {
     static_assert(C == 2048, "32 bins per lane");
-    constexpr int PQ = po(64);  // pidx step of one q (64 bins)
-    const int ob = lane + (lane >> 4);                        // pidx(l)
-    const int pbase = PQ - lane - ((lane + 15) >> 4);         // pidx(C - l - 64 q) = pbase + PQ (31 - q)
+    constexpr int PQ = 64;  // index step of one q (U in the plain layout)
+    const int ob = lane;                  // b = l + 64 q
+    const int pbase = PQ - lane;          // C - b = pbase + PQ (31 - q)
     f2 y[32];
 #pragma unroll
     for (int q = 0; q < 32; q++) {
@@ -1174,26 +1174,37 @@ __global__ void __launch_bounds__(1024, 1) k_frame16w(tdoa_kparams kp, tdoa_kout
         frame16_forward<C>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N);
         if (fr == diag_fr)
             F16W_MARK();  // forward transforms done
-        // ---- 2. split + unit normalisation in place: thread b writes U_m[b]
-        // and U_m[C - b] over the Z slots it read (b = 0: U_m[0], U_m[C])
+        // ---- 2. split + unit normalisation: thread b reads Z_m[b], Z_m[C - b]
+        // (pidx layout), then, after a barrier, writes U_m[b] and U_m[C - b]
+        // at their plain indices (b = 0: U_m[0], U_m[C]): the pairs' lane-
+        // consecutive reads of the plain layout are bank-conflict free
         {
             const int b = tid;
             const f2 wb = tw2[b];
-            const int pb = pidx(b), pr = pidx((C - b) & (C - 1)), pw = pidx(C - b);
+            const int pb = pidx(b), pr = pidx((C - b) & (C - 1));
+            f2 ub[M], un[M];
 #pragma unroll
             for (int m = 0; m < M; m++) {
-                f2 *zb = bufs + m * SLOT;
+                const f2 *zb = bufs + m * SLOT;
                 const f2 z = F16_LD(zb + pb), zp = F16_LD(zb + pr);
                 const f2 e = c_addconj(z, zp);
                 const f2 od = c_mul(c_subconj(z, zp), wb);
-                zb[pb] = c_unit(c_add_mi(e, od), e2);
-                zb[pw] = c_unit(c_conj_add_i(e, od), e2);
+                ub[m] = c_unit(c_add_mi(e, od), e2);
+                un[m] = c_unit(c_conj_add_i(e, od), e2);
             }
+            f2 uh = f2{0.0f, 0.0f};
             if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
-                f2 *zh = bufs + tid * SLOT + pidx(C / 2);
-                const f2 v = *zh;
-                *zh = c_unit(f2{2.0f * v.x, -2.0f * v.y}, e2);
+                const f2 v = F16_LD(bufs + tid * SLOT + pidx(C / 2));
+                uh = c_unit(f2{2.0f * v.x, -2.0f * v.y}, e2);
             }
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                bufs[m * SLOT + b] = ub[m];
+                bufs[m * SLOT + C - b] = un[m];
+            }
+            if (tid < M)
+                bufs[tid * SLOT + C / 2] = uh;
         }
         __syncthreads();
         if (fr == diag_fr)
