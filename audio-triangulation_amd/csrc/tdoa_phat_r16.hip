@@ -621,9 +621,75 @@ __device__ __forceinline__ const tdoa_kout *kernarg_out()
     return reinterpret_cast<const tdoa_kout *>(kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
 }
 
+// One pair's outputs from one wave: lane l holds the raw scores sa, sb at
+// lags ka, kb (valid where oka / okb).  The first maximum (the lowest lag wins
+// ties) by keys to every lane, then the lag prior (correlations.c:20-33
+// semantics on float scores), scores / weighted scores, the compact weighted
+// scratch of k_grid_bb, the least-squares peak scores and the lag.
+__device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const tdoa_kout &out,
+                                                 const float *priorl, int *lagl, int64_t fr, int P, int p,
+                                                 int ka, int kb, bool oka, bool okb, float sa, float sb,
+                                                 bool lane0)
+{
+    const int K = kp.K, S = kp.S;
+    int bkey = INT_MIN, bk = INT_MAX;
+    if (oka) {
+        bkey = fkey(sa);
+        bk = ka;
+    }
+    if (okb && fkey(sb) > bkey) {
+        bkey = fkey(sb);
+        bk = kb;
+    }
+    wave_argmax_key(bkey, bk);
+    bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);  // NaN scores: keep the index in range
+    const size_t gb = (size_t)(fr * P + p) * K;
+    // compact scratch for k_grid_bb: only lags [lo, lo + w) of the pair
+    float *wc = kernarg_out()->weighted_c;
+    const int wlo = kp.wc_lo[p], ww = kp.wc_w[p];
+    float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + kp.wc_off[p] - wlo : nullptr;
+    if (oka) {
+        const int dd = ka > bk ? ka - bk : bk - ka;
+        const float wa = sa * priorl[dd];
+        if (out.scores_f)
+            out.scores_f[gb + ka] = sa;
+        if (out.weighted_f)
+            out.weighted_f[gb + ka] = wa;
+        if (wcp && ka >= wlo && ka < wlo + ww)
+            wcp[ka] = wa;
+    }
+    if (okb) {
+        const int dd = kb > bk ? kb - bk : bk - kb;
+        const float wb = sb * priorl[dd];
+        if (out.scores_f)
+            out.scores_f[gb + kb] = sb;
+        if (out.weighted_f)
+            out.weighted_f[gb + kb] = wb;
+        if (wcp && kb >= wlo && kb < wlo + ww)
+            wcp[kb] = wb;
+    }
+    if (float *pk3 = kernarg_out()->peak3) {
+        // the least-squares refinement's raw scores around the peak: the
+        // lanes holding lags bk - 1 .. bk + 1 store them
+        float *dst = pk3 + (size_t)(fr * P + p) * 3 + 1 - bk;
+        if (oka && ka >= bk - 1 && ka <= bk + 1)
+            dst[ka] = sa;
+        if (okb && kb >= bk - 1 && kb <= bk + 1)
+            dst[kb] = sb;
+    }
+    if (lane0) {
+        out.lags[fr * P + p] = bk - S;
+        lagl[p] = bk - S;
+    }
+}
+
 // (kp, out) must stay the first two parameters: kernarg_out() reads `out`
 // at its kernarg offset
-template <int C, int M>
+// DEFER: pass 3 leaves each pair's raw scores in LDS (scl, [P][K] floats)
+// and one epilogue after the last round runs every pair's argmax and outputs,
+// a wave per pair in parallel (in-round, that chain ran on one wave per group
+// while the workgroup waited at the round's closing barrier)
+template <int C, int M, bool DEFER>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, int64_t B,
                                                      float e2)
@@ -641,6 +707,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
     float *priorl = (float *)(ttl + 3 * 16 * 16);  // [128] the lag prior (K <= 127)
     f2 *tw3 = (f2 *)(priorl + 128);  // [R1][64] pass-3 twiddles per lane (row 0 unused)
+    float *scl = (float *)(tw3 + R1 * 64);  // DEFER: [P][K] raw scores of the frame
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -791,12 +858,16 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             dftp<16, true, false>(v);
         }
         __syncthreads();
+        if (fr == diag_fr)
+            F16_MARK();
         if (on) {
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 buf[17 * jl + r] = v[brev<16>(r)];
         }
         __syncthreads();
+        if (fr == diag_fr)
+            F16_MARK();
         // pass 2: outputs r'' in {0, 1, 14, 15} only
         const int k = jl & 15;
         f2 x0 = f2{0, 0}, x1 = f2{0, 0}, x14 = f2{0, 0}, x15 = f2{0, 0};
@@ -817,6 +888,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             x15 = x15 + (r ? dif_tw<false>(d0, d1, 4 * r) : d0 - d1);
         }
         __syncthreads();
+        if (fr == diag_fr)
+            F16_MARK();
         if (on) {
             const int o = pidx((jl >> 4) * 64 + k);  // + po(16 c) = 17 c
             buf[o] = x0;
@@ -825,6 +898,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             buf[o + 51] = x15;
         }
         __syncthreads();
+        if (fr == diag_fr)
+            F16_MARK();
         // pass 3 by one wave of the group, one output per column.  Waves of a
         // workgroup go to SIMD (wave index mod 4): the group's wave P3W lands
         // the G pass-3 waves evenly on the four SIMDs (the group's first wave
@@ -845,61 +920,32 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
             const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
             const float sa = y.x * invL, sb = y.y * invL;
-            // first maximum (the lowest lag wins ties), by keys to every lane
-            int bkey = INT_MIN, bk = INT_MAX;
-            if (oka) {
-                bkey = fkey(sa);
-                bk = ka;
-            }
-            if (okb && fkey(sb) > bkey) {
-                bkey = fkey(sb);
-                bk = kb;
-            }
-            wave_argmax_key(bkey, bk);
-            bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);
-            const size_t gb = (size_t)(fr * P + p) * K;
-            // compact scratch for k_grid_bb: only lags [lo, lo + w) of the pair
-            float *wc = kernarg_out()->weighted_c;
-            const int wlo = kp.wc_lo[p], ww = kp.wc_w[p];
-            float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + kp.wc_off[p] - wlo : nullptr;
-            if (oka) {
-                const int dd = ka > bk ? ka - bk : bk - ka;
-                const float wa = sa * priorl[dd];
-                if (out.scores_f)
-                    out.scores_f[gb + ka] = sa;
-                if (out.weighted_f)
-                    out.weighted_f[gb + ka] = wa;
-                if (wcp && ka >= wlo && ka < wlo + ww)
-                    wcp[ka] = wa;
-            }
-            if (okb) {
-                const int dd = kb > bk ? kb - bk : bk - kb;
-                const float wb = sb * priorl[dd];
-                if (out.scores_f)
-                    out.scores_f[gb + kb] = sb;
-                if (out.weighted_f)
-                    out.weighted_f[gb + kb] = wb;
-                if (wcp && kb >= wlo && kb < wlo + ww)
-                    wcp[kb] = wb;
-            }
-            if (float *pk3 = kernarg_out()->peak3) {
-                // the least-squares refinement's raw scores around the peak:
-                // the lanes holding lags bk - 1 .. bk + 1 store them
-                float *dst = pk3 + (size_t)(fr * P + p) * 3 + 1 - bk;
-                if (oka && ka >= bk - 1 && ka <= bk + 1)
-                    dst[ka] = sa;
-                if (okb && kb >= bk - 1 && kb <= bk + 1)
-                    dst[kb] = sb;
-            }
-            if (l == 0) {
-                out.lags[fr * P + p] = bk - S;
-                lagl[p] = bk - S;
+            if constexpr (DEFER) {
+                if (oka)
+                    scl[p * K + ka] = sa;
+                if (okb)
+                    scl[p * K + kb] = sb;
+            } else {
+                frame16_pair_out(kp, out, priorl, lagl, fr, P, p, ka, kb, oka, okb, sa, sb, l == 0);
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
         if (fr == diag_fr)
             F16_MARK();
     });
+    if constexpr (DEFER) {
+        // every pair's argmax and outputs, wave w: pairs w, w + 16 (lane l:
+        // lags l and l + 64, K <= 127)
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
+        for (int p = wv; p < P; p += 16) {
+            const bool oka = ln < K, okb = ln + 64 < K;
+            const float sa = oka ? scl[p * K + ln] : 0.0f, sb = okb ? scl[p * K + ln + 64] : 0.0f;
+            frame16_pair_out(kp, out, priorl, lagl, fr, P, p, ln, ln + 64, oka, okb, sa, sb, ln == 0);
+        }
+        __syncthreads();  // lagl complete for the gate; scl free for the next frame
+        if (fr == diag_fr)
+            F16_MARK();
+    }
     if (tid == 0 && out.gate) {
         int tot = 0;
         for (int q = 0; q < P; q++)
@@ -927,12 +973,26 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 {
     if (B <= 0)
         return 0;
-    const size_t lds = frame16_lds_base<C>();
-    const int res = tdoa_resident_blocks((const void *)k_frame16<C, M>, 1024, lds);
+    // the deferred pair outputs when the frame's [P][K] scores fit next to the
+    // buffers (config 4: 10.4 KiB of 13.3 free; TDOA_F16_DEFER=0 keeps them in-round)
+    constexpr int P = M * (M - 1) / 2;
+    static const bool allow = [] {
+        const char *e = getenv("TDOA_F16_DEFER");
+        return !(e && !strcmp(e, "0"));
+    }();
+    const size_t lds_defer = frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float);
+    const bool defer = allow && lds_defer <= 160 * 1024;
+    const void *fn = defer ? (const void *)k_frame16<C, M, true> : (const void *)k_frame16<C, M, false>;
+    const size_t lds = defer ? lds_defer : frame16_lds_base<C>();
+    const int res = tdoa_resident_blocks(fn, 1024, lds);
     if (res < 1)
         return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
     const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
-    hipLaunchKernelGGL((k_frame16<C, M>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+    if (defer)
+        hipLaunchKernelGGL((k_frame16<C, M, true>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+    else
+        hipLaunchKernelGGL((k_frame16<C, M, false>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B,
+                           e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];

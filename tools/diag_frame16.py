@@ -36,7 +36,7 @@ st = st[st[:, 0] > 0]
 G = 16384 // N
 P = M * (M - 1) // 2
 R = (P + G - 1) // G
-wave_kernel = cfg == 4 and os.environ.get("TDOA_F16", "w") != "grp"  # k_frame16w
+wave_kernel = cfg == 4 and os.environ.get("TDOA_F16", "grp") == "w"  # k_frame16w
 if wave_kernel:
     # k_frame16w: start, forward, split, then one stamp per pair of the wave
     # (waves 0-11 run two pairs, 12-15 one: their stamp 4 stays 0)
@@ -53,7 +53,10 @@ if wave_kernel:
         e2 = np.median(sw[:, 4] - sw[:, 2]) if wi < P - 16 else float("nan")
         print(f"  wave {wi:2d}: {e1:8.0f} {e2:8.0f}")
 else:
-    names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} inv"] for r in range(R)], [])
+    names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} p1 dft", f"r{r} p1 wr", f"r{r} p2 dft",
+                                                   f"r{r} p2 wr", f"r{r} p3"] for r in range(R)], [])
+    if os.environ.get("TDOA_F16_DEFER", "1") != "0":
+        names.append("epilogue")  # the deferred pair outputs
 n = len(names)
 print(f"config {cfg}: M={M} N={N} P={P} G={G} rounds={R}, waves {len(st)}")
 life = st[:, 29] - st[:, 0]

@@ -21,6 +21,7 @@ __global__ void __launch_bounds__(1024) k_rate(float *out, unsigned long long *c
         u[i] = t + i;
     }
     const f2 m = f2{1.0001f, 0.9999f}, c = f2{0.5f, 0.25f};
+    const unsigned long long msk = __builtin_amdgcn_ballot_w64((t & 8) != 0);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < iters; k++) {
 #pragma unroll
@@ -33,8 +34,24 @@ __global__ void __launch_bounds__(1024) k_rate(float *out, unsigned long long *c
                     asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
                 else if (KIND == 2)
                     asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s[i]) : "v"(m.x), "v"(c.x));
-                else
+                else if (KIND == 3)
                     asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(t));
+                else if (KIND == 4)  // lane-half exchange of two registers
+                    asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(s[i]), "+v"(u[i]));
+                else if (KIND == 5)
+                    asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(s[i]), "+v"(u[i]));
+                else if (KIND == 6)  // DPP-sourced add (row_ror:8)
+                    asm volatile("v_add_f32_dpp %0, %1, %0 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(s[i]) : "v"(c.x));
+                else if (KIND == 7)
+                    asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(s[i]) : "v"(c.x), "s"(msk));
+                else if (KIND == 10)  // DPP move (row_ror:8)
+                    asm volatile("v_mov_b32_dpp %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(s[i]));
+                else if (KIND == 11)  // lane-select by a per-lane bit: v_bfi (mask in a VGPR)
+                    asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(u[i]) : "v"(t), "v"(u[(i + 1) % C]));
+                else if (KIND == 8)  // complex product by an SGPR constant (the c_mul_s pair)
+                    asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel_hi:[0,1]\n\tv_pk_fma_f32 %0, %0, %1, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "+v"(a[i]) : "s"(m));
+                else  // a VALU op followed by s_nop 0 (the inline-asm boundary padding)
+                    asm volatile("v_pk_add_f32 %0, %0, %1\n\ts_nop 0" : "+v"(a[i]) : "v"(c));
             }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -85,5 +102,15 @@ int main()
     run<2, 16>(cus, out, cyc, "v_fma_f32");
     run<3, 1>(cus, out, cyc, "v_add_u32");
     run<3, 16>(cus, out, cyc, "v_add_u32");
+    run<7, 8>(cus, out, cyc, "cndmask_e64");
+    run<10, 8>(cus, out, cyc, "v_mov_dpp");
+    run<11, 8>(cus, out, cyc, "v_bfi_b32");
+    return 0;
+    run<4, 8>(cus, out, cyc, "permlane32");
+    run<5, 8>(cus, out, cyc, "permlane16");
+    run<6, 8>(cus, out, cyc, "v_add_f32_dpp");
+    run<7, 8>(cus, out, cyc, "v_cndmask");
+    run<8, 8>(cus, out, cyc, "pk_mul+pk_fma");
+    run<9, 8>(cus, out, cyc, "pk_add+s_nop");
     return 0;
 }
