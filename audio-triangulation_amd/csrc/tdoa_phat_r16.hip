@@ -621,65 +621,87 @@ __device__ __forceinline__ const tdoa_kout *kernarg_out()
     return reinterpret_cast<const tdoa_kout *>(kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
 }
 
-// One pair's outputs from one wave: lane l holds the raw scores sa, sb at
-// lags ka, kb (valid where oka / okb).  The first maximum (the lowest lag wins
-// ties) by keys to every lane, then the lag prior (correlations.c:20-33
-// semantics on float scores), scores / weighted scores, the compact weighted
-// scratch of k_grid_bb, the least-squares peak scores and the lag.
+// The outputs of NP pairs from one wave (NP = 2: two independent argmax
+// chains interleaved): lane l holds pair h's raw scores sa[h], sb[h] at lags
+// ka, kb (valid where oka / okb; on[h] false: no pair h).  The first maximum
+// (the lowest lag wins ties) by keys to every lane, then the lag prior
+// (correlations.c:20-33 semantics on float scores), scores / weighted scores,
+// the compact weighted scratch of k_grid_bb, the least-squares peak scores and
+// the lag.  wlo, ww, woff: each pair's compact-scratch range (kp.wc_lo /
+// wc_w / wc_off), passed in: a kp byte indexed by a runtime pair is a VMEM
+// load whose vmcnt wait would also wait for the next frame's prefetched words.
+template <int NP>
 __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const tdoa_kout &out,
-                                                 const float *priorl, int *lagl, int64_t fr, int P, int p,
-                                                 int ka, int kb, bool oka, bool okb, float sa, float sb,
-                                                 bool lane0)
+                                                 const float *priorl, int *lagl, int64_t fr, int P,
+                                                 const int (&p)[NP], const bool (&on)[NP], int ka, int kb,
+                                                 bool oka, bool okb, const float (&sa)[NP], const float (&sb)[NP],
+                                                 bool lane0, const int (&wlo)[NP], const int (&ww)[NP],
+                                                 const int (&woff)[NP])
 {
     const int K = kp.K, S = kp.S;
-    int bkey = INT_MIN, bk = INT_MAX;
-    if (oka) {
-        bkey = fkey(sa);
-        bk = ka;
+    int bkey[NP], bk[NP];
+#pragma unroll
+    for (int h = 0; h < NP; h++) {
+        bkey[h] = INT_MIN;
+        bk[h] = INT_MAX;
+        if (oka) {
+            bkey[h] = fkey(sa[h]);
+            bk[h] = ka;
+        }
+        if (okb && fkey(sb[h]) > bkey[h]) {
+            bkey[h] = fkey(sb[h]);
+            bk[h] = kb;
+        }
     }
-    if (okb && fkey(sb) > bkey) {
-        bkey = fkey(sb);
-        bk = kb;
-    }
-    wave_argmax_key(bkey, bk);
-    bk = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);  // NaN scores: keep the index in range
-    const size_t gb = (size_t)(fr * P + p) * K;
-    // compact scratch for k_grid_bb: only lags [lo, lo + w) of the pair
+    int mk[NP];
+#pragma unroll
+    for (int h = 0; h < NP; h++)
+        mk[h] = wave_reduce<true>(bkey[h]);
+#pragma unroll
+    for (int h = 0; h < NP; h++)
+        bk[h] = wave_reduce<false>(bkey[h] == mk[h] ? bk[h] : INT_MAX);
     float *wc = kernarg_out()->weighted_c;
-    const int wlo = kp.wc_lo[p], ww = kp.wc_w[p];
-    float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + kp.wc_off[p] - wlo : nullptr;
-    if (oka) {
-        const int dd = ka > bk ? ka - bk : bk - ka;
-        const float wa = sa * priorl[dd];
-        if (out.scores_f)
-            out.scores_f[gb + ka] = sa;
-        if (out.weighted_f)
-            out.weighted_f[gb + ka] = wa;
-        if (wcp && ka >= wlo && ka < wlo + ww)
-            wcp[ka] = wa;
-    }
-    if (okb) {
-        const int dd = kb > bk ? kb - bk : bk - kb;
-        const float wb = sb * priorl[dd];
-        if (out.scores_f)
-            out.scores_f[gb + kb] = sb;
-        if (out.weighted_f)
-            out.weighted_f[gb + kb] = wb;
-        if (wcp && kb >= wlo && kb < wlo + ww)
-            wcp[kb] = wb;
-    }
-    if (float *pk3 = kernarg_out()->peak3) {
-        // the least-squares refinement's raw scores around the peak: the
-        // lanes holding lags bk - 1 .. bk + 1 store them
-        float *dst = pk3 + (size_t)(fr * P + p) * 3 + 1 - bk;
-        if (oka && ka >= bk - 1 && ka <= bk + 1)
-            dst[ka] = sa;
-        if (okb && kb >= bk - 1 && kb <= bk + 1)
-            dst[kb] = sb;
-    }
-    if (lane0) {
-        out.lags[fr * P + p] = bk - S;
-        lagl[p] = bk - S;
+    float *pk3 = kernarg_out()->peak3;
+#pragma unroll
+    for (int h = 0; h < NP; h++) {
+        if (!on[h])
+            break;
+        const int b = bk[h] < 0 ? 0 : (bk[h] >= K ? K - 1 : bk[h]);  // NaN scores: keep the index in range
+        const size_t gb = (size_t)(fr * P + p[h]) * K;
+        float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + woff[h] - wlo[h] : nullptr;
+        if (oka) {
+            const int dd = ka > b ? ka - b : b - ka;
+            const float wa = sa[h] * priorl[dd];
+            if (out.scores_f)
+                out.scores_f[gb + ka] = sa[h];
+            if (out.weighted_f)
+                out.weighted_f[gb + ka] = wa;
+            if (wcp && ka >= wlo[h] && ka < wlo[h] + ww[h])
+                wcp[ka] = wa;
+        }
+        if (okb) {
+            const int dd = kb > b ? kb - b : b - kb;
+            const float wb = sb[h] * priorl[dd];
+            if (out.scores_f)
+                out.scores_f[gb + kb] = sb[h];
+            if (out.weighted_f)
+                out.weighted_f[gb + kb] = wb;
+            if (wcp && kb >= wlo[h] && kb < wlo[h] + ww[h])
+                wcp[kb] = wb;
+        }
+        if (pk3) {
+            // the least-squares refinement's raw scores around the peak: the
+            // lanes holding lags b - 1 .. b + 1 store them
+            float *dst = pk3 + (size_t)(fr * P + p[h]) * 3 + 1 - b;
+            if (oka && ka >= b - 1 && ka <= b + 1)
+                dst[ka] = sa[h];
+            if (okb && kb >= b - 1 && kb <= b + 1)
+                dst[kb] = sb[h];
+        }
+        if (lane0) {
+            out.lags[fr * P + p[h]] = b - S;
+            lagl[p[h]] = b - S;
+        }
     }
 }
 
@@ -730,6 +752,18 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
     const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
+    // DEFER: the compact-scratch ranges of this wave's epilogue pairs w, w + 16
+    int ep_lo[2] = {0, 0}, ep_w[2] = {0, 0}, ep_off[2] = {0, 0};
+    if constexpr (DEFER) {
+        const int w0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int q = w0 + 16 * h < P ? w0 + 16 * h : 0;
+            ep_lo[h] = __builtin_amdgcn_readfirstlane(kp.wc_lo[q]);
+            ep_w[h] = __builtin_amdgcn_readfirstlane(kp.wc_w[q]);
+            ep_off[h] = __builtin_amdgcn_readfirstlane(kp.wc_off[q]);
+        }
+    }
 #ifdef TDOA_DIAG
     unsigned long long stamp[32] = {};
     int nst = 0;
@@ -926,7 +960,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 if (okb)
                     scl[p * K + kb] = sb;
             } else {
-                frame16_pair_out(kp, out, priorl, lagl, fr, P, p, ka, kb, oka, okb, sa, sb, l == 0);
+                const int pp[1] = {p}, lo[1] = {kp.wc_lo[p]}, wd[1] = {kp.wc_w[p]}, of[1] = {kp.wc_off[p]};
+                const bool on1[1] = {true};
+                const float a1[1] = {sa}, b1[1] = {sb};
+                frame16_pair_out<1>(kp, out, priorl, lagl, fr, P, pp, on1, ka, kb, oka, okb, a1, b1, l == 0, lo, wd,
+                                    of);
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
@@ -937,11 +975,19 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // every pair's argmax and outputs, wave w: pairs w, w + 16 (lane l:
         // lags l and l + 64, K <= 127)
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
-        for (int p = wv; p < P; p += 16) {
-            const bool oka = ln < K, okb = ln + 64 < K;
-            const float sa = oka ? scl[p * K + ln] : 0.0f, sb = okb ? scl[p * K + ln + 64] : 0.0f;
-            frame16_pair_out(kp, out, priorl, lagl, fr, P, p, ln, ln + 64, oka, okb, sa, sb, ln == 0);
+        static_assert(P <= 32, "two epilogue pairs per wave at most");
+        const bool oka = ln < K, okb = ln + 64 < K;
+        const int pp[2] = {wv, wv + 16 < P ? wv + 16 : wv};
+        const bool on2[2] = {wv < P, wv + 16 < P};
+        float sa[2], sb[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            sa[h] = oka ? scl[pp[h] * K + ln] : 0.0f;
+            sb[h] = okb ? scl[pp[h] * K + ln + 64] : 0.0f;
         }
+        if (on2[0])
+            frame16_pair_out<2>(kp, out, priorl, lagl, fr, P, pp, on2, ln, ln + 64, oka, okb, sa, sb, ln == 0, ep_lo,
+                                ep_w, ep_off);
         __syncthreads();  // lagl complete for the gate; scl free for the next frame
         if (fr == diag_fr)
             F16_MARK();
@@ -973,15 +1019,17 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 {
     if (B <= 0)
         return 0;
-    // the deferred pair outputs when the frame's [P][K] scores fit next to the
-    // buffers (config 4: 10.4 KiB of 13.3 free; TDOA_F16_DEFER=0 keeps them in-round)
-    constexpr int P = M * (M - 1) / 2;
-    static const bool allow = [] {
+    // the deferred pair outputs when the frame has three or more pair rounds
+    // and its [P][K] scores fit next to the buffers (config 4: 10.4 KiB of 13.3
+    // free; 98.7 vs 103.4 ms per step; config 3, two rounds: 3.88 vs 3.86 ms,
+    // kept in-round).  TDOA_F16_DEFER=0 / 1 forces either.
+    constexpr int P = M * (M - 1) / 2, G = 16384 / C, ROUNDS = (P + G - 1) / G;
+    static const int force = [] {
         const char *e = getenv("TDOA_F16_DEFER");
-        return !(e && !strcmp(e, "0"));
+        return e ? (strcmp(e, "0") ? 1 : 0) : -1;
     }();
     const size_t lds_defer = frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float);
-    const bool defer = allow && lds_defer <= 160 * 1024;
+    const bool defer = (force < 0 ? ROUNDS >= 3 : force == 1) && lds_defer <= 160 * 1024;
     const void *fn = defer ? (const void *)k_frame16<C, M, true> : (const void *)k_frame16<C, M, false>;
     const size_t lds = defer ? lds_defer : frame16_lds_base<C>();
     const int res = tdoa_resident_blocks(fn, 1024, lds);
