@@ -707,11 +707,14 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
 
 // (kp, out) must stay the first two parameters: kernarg_out() reads `out`
 // at its kernarg offset
-// DEFER: pass 3 leaves each pair's raw scores in LDS (scl, [P][K] floats)
-// and one epilogue after the last round runs every pair's argmax and outputs,
-// a wave per pair in parallel (in-round, that chain ran on one wave per group
-// while the workgroup waited at the round's closing barrier)
-template <int C, int M, bool DEFER>
+// DM (deferred outputs): 0 -- every round's pass 3 runs its pair's argmax and
+// outputs (one wave per group, the workgroup waiting at the round's closing
+// barrier); 1 -- pass 3 leaves the raw scores in LDS (scl, [P][K] floats) and
+// one epilogue after the last round runs every pair's argmax and outputs, a
+// wave per pair in parallel.  (Running the earlier rounds' epilogue on the
+// last round's idle groups instead measured slower at config 3: 3.865 vs
+// 3.826 ms per step.)
+template <int C, int M, int DM>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, int64_t B,
                                                      float e2)
@@ -721,6 +724,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     constexpr int P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G;
     constexpr int WPG = T / 64;  // waves per group (4 or 2)
     static_assert(WPG == 2 || WPG == 4, "group of 2 or 4 waves");
+    static_assert(DM == 0 || DM == 1, "deferred-output mode");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *bufs = (f2 *)smem;                    // [G][BUF]
     f2 *xhalf = bufs + G * BUF;               // [G] U_m[C / 2]
@@ -729,7 +733,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
     float *priorl = (float *)(ttl + 3 * 16 * 16);  // [128] the lag prior (K <= 127)
     f2 *tw3 = (f2 *)(priorl + 128);  // [R1][64] pass-3 twiddles per lane (row 0 unused)
-    float *scl = (float *)(tw3 + R1 * 64);  // DEFER: [P][K] raw scores of the frame
+    float *scl = (float *)(tw3 + R1 * 64);  // DM 1: [P][K] raw scores of the frame
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -752,9 +756,21 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
     const int P3W = (g / (4 / WPG)) % WPG;  // the group's pass-3 wave: SIMD (g WPG + P3W) mod 4
-    // DEFER: the compact-scratch ranges of this wave's epilogue pairs w, w + 16
+    // the compact-scratch ranges (kp.wc_lo / wc_w / wc_off) of every pair this
+    // wave outputs, read once here: a kp byte indexed by a runtime pair is a
+    // VMEM load whose vmcnt wait would also wait for the next frame's words.
+    // rl_*[r]: round r's pair of the group (pass 3); ep_*: the epilogue's pairs
+    int rl_lo[ROUNDS], rl_w[ROUNDS], rl_off[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; r++) {
+        const int q = r * G + g < P ? r * G + g : 0;
+        rl_lo[r] = __builtin_amdgcn_readfirstlane(kp.wc_lo[q]);
+        rl_w[r] = __builtin_amdgcn_readfirstlane(kp.wc_w[q]);
+        rl_off[r] = __builtin_amdgcn_readfirstlane(kp.wc_off[q]);
+    }
+    // DM 1: the epilogue's pairs w, w + 16
     int ep_lo[2] = {0, 0}, ep_w[2] = {0, 0}, ep_off[2] = {0, 0};
-    if constexpr (DEFER) {
+    if constexpr (DM == 1) {
         const int w0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -954,13 +970,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
             const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
             const float sa = y.x * invL, sb = y.y * invL;
-            if constexpr (DEFER) {
+            constexpr int RI = decltype(rc)::value;
+            if constexpr (DM == 1) {
                 if (oka)
                     scl[p * K + ka] = sa;
                 if (okb)
                     scl[p * K + kb] = sb;
             } else {
-                const int pp[1] = {p}, lo[1] = {kp.wc_lo[p]}, wd[1] = {kp.wc_w[p]}, of[1] = {kp.wc_off[p]};
+                const int pp[1] = {p}, lo[1] = {rl_lo[RI]}, wd[1] = {rl_w[RI]}, of[1] = {rl_off[RI]};
                 const bool on1[1] = {true};
                 const float a1[1] = {sa}, b1[1] = {sb};
                 frame16_pair_out<1>(kp, out, priorl, lagl, fr, P, pp, on1, ka, kb, oka, okb, a1, b1, l == 0, lo, wd,
@@ -971,7 +988,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (fr == diag_fr)
             F16_MARK();
     });
-    if constexpr (DEFER) {
+    if constexpr (DM == 1) {
         // every pair's argmax and outputs, wave w: pairs w, w + 16 (lane l:
         // lags l and l + 64, K <= 127)
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
@@ -1019,28 +1036,27 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 {
     if (B <= 0)
         return 0;
-    // the deferred pair outputs when the frame has three or more pair rounds
-    // and its [P][K] scores fit next to the buffers (config 4: 10.4 KiB of 13.3
-    // free; 98.7 vs 103.4 ms per step; config 3, two rounds: 3.88 vs 3.86 ms,
-    // kept in-round).  TDOA_F16_DEFER=0 / 1 forces either.
+    // deferred pair outputs (DM 1) at three or more pair rounds when the
+    // frame's [P][K] scores fit next to the buffers (config 4: 10.4 KiB of 13.3
+    // free; 98.5 vs 104.4 ms per step; config 3, two rounds: 3.87 vs 3.83 ms)
     constexpr int P = M * (M - 1) / 2, G = 16384 / C, ROUNDS = (P + G - 1) / G;
+    // TDOA_F16_DEFER=0 / 1 forces a mode
     static const int force = [] {
         const char *e = getenv("TDOA_F16_DEFER");
-        return e ? (strcmp(e, "0") ? 1 : 0) : -1;
+        return e ? atoi(e) : -1;
     }();
     const size_t lds_defer = frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float);
-    const bool defer = (force < 0 ? ROUNDS >= 3 : force == 1) && lds_defer <= 160 * 1024;
-    const void *fn = defer ? (const void *)k_frame16<C, M, true> : (const void *)k_frame16<C, M, false>;
+    const bool defer = (force >= 0 ? force == 1 : ROUNDS >= 3) && lds_defer <= 160 * 1024;
+    const void *fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
     const size_t lds = defer ? lds_defer : frame16_lds_base<C>();
     const int res = tdoa_resident_blocks(fn, 1024, lds);
     if (res < 1)
         return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
     const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
     if (defer)
-        hipLaunchKernelGGL((k_frame16<C, M, true>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+        hipLaunchKernelGGL((k_frame16<C, M, 1>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
     else
-        hipLaunchKernelGGL((k_frame16<C, M, false>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B,
-                           e2);
+        hipLaunchKernelGGL((k_frame16<C, M, 0>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];

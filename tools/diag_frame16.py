@@ -55,8 +55,9 @@ if wave_kernel:
 else:
     names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} p1 dft", f"r{r} p1 wr", f"r{r} p2 dft",
                                                    f"r{r} p2 wr", f"r{r} p3"] for r in range(R)], [])
-    if os.environ.get("TDOA_F16_DEFER", "1") != "0":
-        names.append("epilogue")  # the deferred pair outputs
+    dm = os.environ.get("TDOA_F16_DEFER", "1" if R >= 3 else "0")
+    if dm == "1":
+        names.append("epilogue")  # the deferred pair outputs (DM 1)
 n = len(names)
 print(f"config {cfg}: M={M} N={N} P={P} G={G} rounds={R}, waves {len(st)}")
 life = st[:, 29] - st[:, 0]
