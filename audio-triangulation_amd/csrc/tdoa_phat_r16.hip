@@ -58,6 +58,18 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 #ifndef F16_VLDS
 #define F16_VLDS 1
 #endif
+// the Q15 window words of config 3's shape (C = 4096) sit in LDS (8 KiB):
+// read from L2 at every frame's start, their latency followed the DC barrier
+template <int C>
+constexpr bool f16_win_lds()
+{
+    return C == 4096;
+}
+__device__ __forceinline__ uint32_t lds_rd_u32(const uint32_t *p)
+{
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    return *(const volatile lds_u32 *)(const lds_u32 *)p;
+}
 #if F16_VLDS
 #define F16_LD(p) lds_rd(p)
 #else
@@ -501,15 +513,19 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 // and three register passes in the group's LDS slot buf): the DC sum of the
 // group's words w, the Q15 window, radix R1 / 16 / 16 Stockham passes; Z[j + T q]
 // ends in buf at pidx(j + T q), after a closing barrier
-template <int C>
+template <int C, bool WL, typename Mark>
 __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, f2 *buf, int *red,
-                                                const f2 *tt, int tid, int g, int j, int pj, int log2N)
+                                                const f2 *tt, int tid, int g, int j, int pj, int log2N, Mark mark)
 {
     constexpr int T = C / 16, R1 = C / 256;
     uint32_t wn[8];
 #pragma unroll
-    for (int s = 0; s < 8; s++)
-        wn[s] = win[j + T * s];
+    for (int s = 0; s < 8; s++) {
+        if constexpr (WL)
+            wn[s] = lds_rd_u32(win + j + T * s);
+        else
+            wn[s] = win[j + T * s];
+    }
     int sum = 0;
 #pragma unroll
     for (int s = 0; s < 8; s++)
@@ -518,6 +534,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
     if ((tid & 63) == 63)
         red[tid >> 6] = sum;
     __syncthreads();
+    mark();
     sum = 0;
 #pragma unroll
     for (int wv = 0; wv < T / 64; wv++)
@@ -559,6 +576,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         }
     }
     __syncthreads();
+    mark();
     {
         const int k = j % R1;
 #pragma unroll
@@ -569,6 +587,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
         dftp<16, false, false>(v);
         __syncthreads();
+    mark();
         // o mod 16 = k < R1: pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16
         const int o = pidx((j / R1) * 16 * R1 + k);
 #pragma unroll
@@ -576,6 +595,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             buf[o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
     }
     __syncthreads();
+    mark();
     {
 #pragma unroll
         for (int r = 0; r < 16; r++)
@@ -585,11 +605,13 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             v[r] = c_mul(v[r], c_mul(F16_LD(tt + 256 + 16 * r + (j & 15)), F16_LD(tt + 512 + 16 * r + (j >> 4))));  // twC
         dftp<16, false, false>(v);
         __syncthreads();
+    mark();
 #pragma unroll
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
             buf[pj + po(T * q)] = v[brev<16>(q)];
     }
     __syncthreads();
+    mark();
 }
 
 // LDS bytes of k_frame16
@@ -598,7 +620,8 @@ constexpr size_t frame16_lds_base()
 {
     constexpr int G = 16384 / C, BUF = C + C / 16;
     return (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
-           3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2);
+           3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2) +
+           (f16_win_lds<C>() ? (size_t)C * 2 : 0);
 }
 
 // The output block read through an opaque kernarg pointer: loads used once
@@ -733,7 +756,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     f2 *ttl = (f2 *)(lagl + TDOA_MAX_PAIRS);  // [3][16][16] the r16 twiddle tables
     float *priorl = (float *)(ttl + 3 * 16 * 16);  // [128] the lag prior (K <= 127)
     f2 *tw3 = (f2 *)(priorl + 128);  // [R1][64] pass-3 twiddles per lane (row 0 unused)
-    float *scl = (float *)(tw3 + R1 * 64);  // DM 1: [P][K] raw scores of the frame
+    uint32_t *winl = (uint32_t *)(tw3 + R1 * 64);  // f16_win_lds: [C / 2] window words
+    float *scl = (float *)(winl + (f16_win_lds<C>() ? C / 2 : 0));  // DM 1: [P][K] raw scores of the frame
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -752,6 +776,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const int r = threadIdx.x >> 6, l = threadIdx.x & 63;
         const f2 t = twC(reinterpret_cast<const f2 *>(kp.r16_tw), r, l < 32 ? l : 64 - l);
         tw3[threadIdx.x] = f2{t.x, l < 32 ? -t.y : t.y};
+    }
+    if constexpr (f16_win_lds<C>()) {
+        for (int i = threadIdx.x; i < C / 2; i += 1024)
+            winl[i] = win[i];
+        __syncthreads();  // the forward reads the window before its first barrier
     }
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
     const int mg = g < M ? g : 0;  // groups without a mic transform mic 0 (unused)
@@ -812,7 +841,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
-    frame16_forward<C>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N);
+    frame16_forward<C, f16_win_lds<C>()>(w, f16_win_lds<C>() ? winl : win, buf, red, tt, tid, g, j, pj, kp.log2N,
+                                         [&] {
+        if (fr == diag_fr)
+            F16_MARK();  // the forward's barriers (diagnostic build)
+    });
     if (fr == diag_fr)
         F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
@@ -960,12 +993,19 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
             // the output index C - m; tw3 holds each lane's factors (conjugated for l < 32)
             const int pl = pidx(l);
-            f2 y = F16_LD(buf + pl);
+            // the R1 terms summed as a tree (a running sum was a dependent
+            // chain of R1 - 1 complex products and adds on the round's critical path)
+            f2 t[R1];
+            t[0] = F16_LD(buf + pl);
 #pragma unroll
-            for (int r = 1; r < R1; r++) {
-                const f2 u = F16_LD(buf + pl + 68 * r);
-                y = y + c_mul(u, F16_LD(tw3 + 64 * r + l));
-            }
+            for (int r = 1; r < R1; r++)
+                t[r] = c_mul(F16_LD(buf + pl + 68 * r), F16_LD(tw3 + 64 * r + l));
+#pragma unroll
+            for (int h = R1 / 2; h >= 1; h >>= 1)
+#pragma unroll
+                for (int r = 0; r < h; r++)
+                    t[r] = t[r] + t[r + h];
+            const f2 y = t[0];
             const int n = l < 32 ? l : -mm;
             const int ka = 2 * n + S, kb = 2 * n + 1 + S;
             const bool oka = ka >= 0 && ka < K, okb = kb >= 0 && kb < K;
@@ -1295,7 +1335,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16w(tdoa_kparams kp, tdoa_kout
 #endif
             F16W_MARK();
         }
-        frame16_forward<C>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N);
+        frame16_forward<C, false>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N, [] {});
         if (fr == diag_fr)
             F16W_MARK();  // forward transforms done
         // ---- 2. split + unit normalisation: thread b reads Z_m[b], Z_m[C - b]

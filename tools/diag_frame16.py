@@ -53,7 +53,10 @@ if wave_kernel:
         e2 = np.median(sw[:, 4] - sw[:, 2]) if wi < P - 16 else float("nan")
         print(f"  wave {wi:2d}: {e1:8.0f} {e2:8.0f}")
 else:
-    names = ["start", "forward", "U regs"] + sum([[f"r{r} Y", f"r{r} p1 dft", f"r{r} p1 wr", f"r{r} p2 dft",
+    # the forward's six barriers (DC sum, pass 1 .. 3 reads / writes), then
+    # its closing mark
+    names = ["start", "fw dc", "fw p1", "fw p2 dft", "fw p2 wr", "fw p3 dft", "fw p3 wr", "forward",
+             "U regs"] + sum([[f"r{r} Y", f"r{r} p1 dft", f"r{r} p1 wr", f"r{r} p2 dft",
                                                    f"r{r} p2 wr", f"r{r} p3"] for r in range(R)], [])
     dm = os.environ.get("TDOA_F16_DEFER", "1" if R >= 3 else "0")
     if dm == "1":
