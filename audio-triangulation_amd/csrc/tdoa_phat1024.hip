@@ -170,6 +170,12 @@ __device__ __forceinline__ f2 lds_f2(const char *base, int off)
     return *reinterpret_cast<const f2 *>(base + off);
 #endif
 }
+// plain LDS read (the grid's gathers: data-dependent addresses, never merged,
+// and free to be scheduled around the other reads of the software pipeline)
+__device__ __forceinline__ f2 lds_f2_plain(const char *base, int off)
+{
+    return *reinterpret_cast<const f2 *>(base + off);
+}
 __device__ __forceinline__ void sts_f2(char *base, int off, f2 v)
 {
     *reinterpret_cast<f2 *>(base + off) = v;
@@ -668,9 +674,9 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 // tuple fields are byte offsets of f2 slots in [p][KPAD]
-                g[i][0] = lds_f2(ws, (int)(qq[i] & 0x3FFu));
-                g[i][1] = lds_f2(ws, P1K_KPAD * 8 + (int)((qq[i] >> 10) & 0x3FFu));
-                g[i][2] = lds_f2(ws, 2 * P1K_KPAD * 8 + (int)(qq[i] >> 20));
+                g[i][0] = lds_f2_plain(ws, (int)(qq[i] & 0x3FFu));
+                g[i][1] = lds_f2_plain(ws, P1K_KPAD * 8 + (int)((qq[i] >> 10) & 0x3FFu));
+                g[i][2] = lds_f2_plain(ws, 2 * P1K_KPAD * 8 + (int)(qq[i] >> 20));
             }
         };
         uint32_t q[4];
