@@ -178,6 +178,27 @@ class Localizer:
               "tdoa_localize_batch")
         return out
 
+    def prepare(self, frames: torch.Tensor, out: dict, stream=None):
+        """A prebuilt localize_into(frames, out, stream): the argument checks and
+        the ctypes output struct are done once, and each call of the returned
+        function enqueues the same tdoa_localize_batch (frames and outputs must
+        stay allocated; they are kept referenced).  For launch loops whose
+        host-side Python would otherwise be on the critical path."""
+        B = self._check_frames(frames)
+        st = stream if stream is not None else torch.cuda.current_stream(self.torch_device)
+        s = self._outputs_struct(out)
+        fn = load().tdoa_localize_batch
+        args = (self._ctx, C.c_void_p(frames.data_ptr()), B, C.byref(s), C.c_void_p(st.cuda_stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc != 0:
+                check(rc, "tdoa_localize_batch")
+            return out
+
+        launch.keep = (frames, out, s, st)
+        return launch
+
     def localize(self, frames: torch.Tensor, scores: bool = False, grid: bool = True,
                  stream=None, ls: bool = False) -> dict:
         out = self.alloc_outputs(self._check_frames(frames), scores=scores, grid=grid, ls=ls)

@@ -115,8 +115,9 @@ def timed(step, steps: int, warmup: int, sync=lambda: None, device=None,
           on_start=None, on_end=None, barrier_fn=None) -> dict:
     """The bench contract's timed region: `warmup` untimed calls of step(k),
     then EXACTLY `steps` calls bracketed by sync + barrier + sync on both
-    sides; the job time is the max over ranks.  on_start / on_end run right
-    inside the bracket (e.g. HIP event records on the launch stream).
+    sides; the job time is the max over ranks.  on_start runs before the opening
+    sync, on_end right after the last step (e.g. HIP event records on the launch
+    stream: the events bracket the K launches, the clock the K steps).
 
     The start is barrier-aligned (every rank leaves the opening barrier
     together); each rank's clock stops right after its OWN closing sync, before
@@ -129,10 +130,10 @@ def timed(step, steps: int, warmup: int, sync=lambda: None, device=None,
         step(k)
     sync()
     bar()
+    if on_start:  # an event record: enqueued before the clock starts
+        on_start()
     sync()
     t0 = time.perf_counter()
-    if on_start:
-        on_start()
     for k in range(steps):
         step(k)
     if on_end:

@@ -341,3 +341,19 @@ def test_long_frames_big_grid_exhaustive():
     assert (got["cell"] == cell).all()
     assert (got["max_Lf"] == mx).all()
     loc.close()
+
+
+def test_prepared_launch_matches_localize_into(phat3):
+    """Localizer.prepare (bench.py's timed loop) enqueues the same launch as
+    localize_into: identical outputs on the same batch."""
+    lut = phat3.lut().reshape(3, 101, 101)
+    fr, _, _ = synth.adc_frames(512, 3, 1024, lut, 46, 0x9E, device="cuda")
+    a = phat3.alloc_outputs(512)
+    b = phat3.alloc_outputs(512)
+    phat3.localize_into(fr, a)
+    run = phat3.prepare(fr, b)
+    run()
+    run()  # a second enqueue of the same prebuilt launch
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
