@@ -92,6 +92,8 @@ __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
 // Lane l holds A row w = l & 15, B column n = l & 15, k = 16 (l >> 4) + j in
 // byte j of its 16-byte operands (A and B pair byte for byte), and C rows
 // 4 (l >> 4) + e of column l & 15.
+constexpr int MF_GR = 4;      // keyed grid: tuple words held per thread (the 16-wave form)
+constexpr int MF_GR_EMA = 5;  // ... and in the 8-wave streaming workgroup (U <= 5 x 512)
 constexpr int MF_PADW = 96;  // zero words each side of a staged row (b reads reach N + 175 samples)
 
 typedef int v4i_mf __attribute__((ext_vector_type(4)));
@@ -243,7 +245,7 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 // The stream states are requested at the kernel's start (ema_prefetch: the
 // thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
 // latency hides behind the staging and the xcorr.
-constexpr int EMA_E = 2;  // state elements per thread: F P K <= EMA_E x threads (host-checked)
+constexpr int EMA_E = 3;  // state elements per thread: F P K <= EMA_E x threads (host-checked)
 
 struct EmaPre {
     int64_t ev[EMA_E];
@@ -504,7 +506,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     DIAG_STAMP(0);
     // single-word tuples (P <= 4): this thread's grid tuples and their first
     // cells, requested now and consumed by the grid solve at the end
-    constexpr int GR = 4;
+    constexpr int GR = EMA ? MF_GR_EMA : MF_GR;  // the 8-wave streaming workgroup holds more tuples per thread
     constexpr bool KEYGRID = TWC == 1;
     uint32_t gq[GR];
     int32_t gc[GR];
@@ -798,11 +800,22 @@ static void direct_geometry(tdoa_kparams &kp, int &threads)
 }
 
 // workgroup shape of k_direct_mfma: F frames per workgroup (one wave per
-// (frame, pair) up to 16 waves) and the 16-B staging chunks per thread
-static void mf_shape(const tdoa_kparams &kp, int &F, int &threads, int &chunks)
+// (frame, pair) up to 16 waves) and the 16-B staging chunks per thread.  The
+// streaming EMA launch (ema) caps the workgroup at 8 waves (its waves loop over
+// the F P (frame, pair) units): config 5's 12-wave workgroups ran 2 per CU, 512
+// at once, for a batch of ~850 -- two generations, the second two-thirds full;
+// at 8 waves, 3 per CU (768 at once).  TDOA_EMA_WAVES=12 keeps the old shape.
+static void mf_shape(const tdoa_kparams &kp, int &F, int &threads, int &chunks, bool ema = false)
 {
+    static const int ema_waves = [] {
+        const char *e = getenv("TDOA_EMA_WAVES");
+        return e ? atoi(e) : 8;
+    }();
     F = kp.P >= 16 ? 1 : 16 / kp.P > 4 ? 4 : 16 / kp.P;
-    threads = 64 * (F * kp.P < 16 ? F * kp.P : 16);
+    int w = F * kp.P < 16 ? F * kp.P : 16;
+    if (ema && ema_waves > 0 && w > ema_waves)
+        w = ema_waves;
+    threads = 64 * w;
     chunks = (F * kp.M * kp.N / 8 + threads - 1) / threads;
 }
 
@@ -826,8 +839,8 @@ bool tdoa_direct_ema_fits(const tdoa_kparams &kp)
     if (!tdoa_direct_fused_grid(kp))
         return false;
     int F, threads, chunks;
-    mf_shape(kp, F, threads, chunks);
-    return F * kp.P * kp.K <= EMA_E * threads;
+    mf_shape(kp, F, threads, chunks, true);
+    return chunks <= 8 && F * kp.P * kp.K <= EMA_E * threads;
 }
 
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
@@ -843,7 +856,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         kp.PADW = MF_PADW;
         kp.RS = kp.N / 2 + 2 * MF_PADW;
         int chunks = 0;
-        mf_shape(kp, kp.F, threads, chunks);
+        mf_shape(kp, kp.F, threads, chunks, ema != nullptr);
         MfTabs tb;
         size_t o = smem_bytes(kp, threads / 64);
         tb.rsum = (int)o;
@@ -856,7 +869,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         // registers, the score table frame-interleaved for four frames, cells in
         // the key's 16 index bits; other shapes (wide geometries with more
         // tuples, grids beyond 65536 cells) take the generic grid
-        const bool keyed = kp.TW == 1 && kp.U <= 4 * threads && kp.F == 4 && kp.G <= 65536;
+        const bool keyed = kp.TW == 1 && kp.U <= (ema ? MF_GR_EMA : MF_GR) * threads && kp.F == 4 && kp.G <= 65536;
         const size_t lds = (o + 15) & ~(size_t)15;
         if (lds > 160 * 1024)
             return tdoa_set_error(-1, "DIRECT: shape needs more than 160 KiB LDS per workgroup");
