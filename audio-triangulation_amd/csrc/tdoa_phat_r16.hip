@@ -58,6 +58,12 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 #ifndef F16_VLDS
 #define F16_VLDS 1
 #endif
+#ifndef F16_TWPOW
+#define F16_TWPOW 1  // the forward's pass-3 twiddles as powers of W_C^j (see frame16_forward)
+#endif
+#ifndef F16_TWPOW2
+#define F16_TWPOW2 0  // the table-read twiddles (forward pass 2, inverse pass 2) as powers too
+#endif
 // the Q15 window words of config 3's shape (C = 4096) sit in LDS (8 KiB):
 // read from L2 at every frame's start, their latency followed the DC barrier
 template <int C>
@@ -582,9 +588,22 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
         for (int r = 0; r < 16; r++)
             v[r] = F16_LD(buf + pj + po(T * r));
+#if F16_TWPOW2
+        {
+            f2 t[16];  // W_C^{16 r k} as powers of W_C^{16 k}
+            t[1] = F16_LD(tt + 512 + 16 + k);
+#pragma unroll
+            for (int r = 2; r < 16; r++)
+                t[r] = (r & 1) ? c_mul(t[r - 1], t[1]) : c_mul(t[r / 2], t[r / 2]);
+#pragma unroll
+            for (int r = 1; r < 16; r++)
+                v[r] = c_mul(v[r], t[r]);
+        }
+#else
 #pragma unroll
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
+#endif
         dftp<16, false, false>(v);
         __syncthreads();
     mark();
@@ -600,9 +619,25 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
         for (int r = 0; r < 16; r++)
             v[r] = F16_LD(buf + pj + po(T * r));
+#if F16_TWPOW
+        {
+            // W_C^{r j}, r = 1..15, as powers of W_C^j (the tables give W_C^j
+            // in one product; then squares and one-step products, depth <= 5):
+            // two LDS reads instead of thirty per thread
+            f2 t[16];
+            t[1] = c_mul(F16_LD(tt + 256 + 16 + (j & 15)), F16_LD(tt + 512 + 16 + (j >> 4)));
+#pragma unroll
+            for (int r = 2; r < 16; r++)
+                t[r] = (r & 1) ? c_mul(t[r - 1], t[1]) : c_mul(t[r / 2], t[r / 2]);
+#pragma unroll
+            for (int r = 1; r < 16; r++)
+                v[r] = c_mul(v[r], t[r]);
+        }
+#else
 #pragma unroll
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], c_mul(F16_LD(tt + 256 + 16 * r + (j & 15)), F16_LD(tt + 512 + 16 * r + (j >> 4))));  // twC
+#endif
         dftp<16, false, false>(v);
         __syncthreads();
     mark();
@@ -954,15 +989,27 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // pass 2: outputs r'' in {0, 1, 14, 15} only
         const int k = jl & 15;
         f2 x0 = f2{0, 0}, x1 = f2{0, 0}, x14 = f2{0, 0}, x15 = f2{0, 0};
+#if F16_TWPOW2
+        f2 t2[16];  // W_256^{r k} as powers of W_256^k
+        if (on) {
+            t2[1] = F16_LD(tt + 16 + k);
+#pragma unroll
+            for (int r = 2; r < 16; r++)
+                t2[r] = (r & 1) ? c_mul(t2[r - 1], t2[1]) : c_mul(t2[r / 2], t2[r / 2]);
+        }
+#define F16_TW256(r) t2[r]
+#else
+#define F16_TW256(r) F16_LD(tt + 16 * (r) + k)
+#endif
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
             f2 l0 = F16_LD(buf + pjl + po(T * r)), l1 = F16_LD(buf + pjl + po(T * (r + 4)));
-            const f2 h0 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 8))), F16_LD(tt + 16 * (r + 8) + k));
-            const f2 h1 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 12))), F16_LD(tt + 16 * (r + 12) + k));
+            const f2 h0 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 8))), F16_TW256(r + 8));
+            const f2 h1 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 12))), F16_TW256(r + 12));
             if (r)
-                l0 = c_mulconj(l0, F16_LD(tt + 16 * r + k));  // tw256
-            l1 = c_mulconj(l1, F16_LD(tt + 16 * (r + 4) + k));
+                l0 = c_mulconj(l0, F16_TW256(r));  // tw256
+            l1 = c_mulconj(l1, F16_TW256(r + 4));
             const f2 a0 = l0 + h0, a1 = l1 + h1;
             const f2 d0 = dif_tw<true>(l0, h0, 2 * r), d1 = dif_tw<true>(l1, h1, 2 * (r + 4));
             x0 = x0 + (a0 + a1);
@@ -970,6 +1017,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             x14 = x14 + (r ? dif_tw<false>(a0, a1, 4 * r) : a0 - a1);
             x15 = x15 + (r ? dif_tw<false>(d0, d1, 4 * r) : d0 - d1);
         }
+#undef F16_TW256
         __syncthreads();
         if (fr == diag_fr)
             F16_MARK();
