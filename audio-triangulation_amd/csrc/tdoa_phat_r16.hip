@@ -61,9 +61,6 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 #ifndef F16_TWPOW
 #define F16_TWPOW 1  // the forward's pass-3 twiddles as powers of W_C^j (see frame16_forward)
 #endif
-#ifndef F16_TWPOW2
-#define F16_TWPOW2 0  // the table-read twiddles (forward pass 2, inverse pass 2) as powers too
-#endif
 // the Q15 window words of config 3's shape (C = 4096) sit in LDS (8 KiB):
 // read from L2 at every frame's start, their latency followed the DC barrier
 template <int C>
@@ -588,22 +585,9 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
         for (int r = 0; r < 16; r++)
             v[r] = F16_LD(buf + pj + po(T * r));
-#if F16_TWPOW2
-        {
-            f2 t[16];  // W_C^{16 r k} as powers of W_C^{16 k}
-            t[1] = F16_LD(tt + 512 + 16 + k);
-#pragma unroll
-            for (int r = 2; r < 16; r++)
-                t[r] = (r & 1) ? c_mul(t[r - 1], t[1]) : c_mul(t[r / 2], t[r / 2]);
-#pragma unroll
-            for (int r = 1; r < 16; r++)
-                v[r] = c_mul(v[r], t[r]);
-        }
-#else
 #pragma unroll
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
-#endif
         dftp<16, false, false>(v);
         __syncthreads();
     mark();
@@ -989,18 +973,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // pass 2: outputs r'' in {0, 1, 14, 15} only
         const int k = jl & 15;
         f2 x0 = f2{0, 0}, x1 = f2{0, 0}, x14 = f2{0, 0}, x15 = f2{0, 0};
-#if F16_TWPOW2
-        f2 t2[16];  // W_256^{r k} as powers of W_256^k
-        if (on) {
-            t2[1] = F16_LD(tt + 16 + k);
-#pragma unroll
-            for (int r = 2; r < 16; r++)
-                t2[r] = (r & 1) ? c_mul(t2[r - 1], t2[1]) : c_mul(t2[r / 2], t2[r / 2]);
-        }
-#define F16_TW256(r) t2[r]
-#else
 #define F16_TW256(r) F16_LD(tt + 16 * (r) + k)
-#endif
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
