@@ -666,7 +666,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         kp.r16_tw = c->d_tw + 2 * N + 2 * (N + 1);
         std::vector<uint8_t> img;
         tdoa_phat1024_image(M, N, c->K, c->U, tw.data(), c->win.data(), c->prior.data(),
-                            c->tuples.data(), img);
+                            c->tuples.data(), c->tuple_cell.data(), img);
         if (!img.empty()) {
             if (hipMalloc(&c->d_p1k_img, img.size()) != hipSuccess ||
                 hipMemcpy(c->d_p1k_img, img.data(), img.size(), hipMemcpyHostToDevice) !=

@@ -282,6 +282,11 @@ __device__ __forceinline__ f2 lds_rd(const f2 *p)
     typedef __attribute__((address_space(3))) f2 lds_f2;
     return *(const volatile lds_f2 *)(const lds_f2 *)p;
 }
+__device__ __forceinline__ uint32_t lds_rd_u32(const uint32_t *p)
+{
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    return *(const volatile lds_u32 *)(const lds_u32 *)p;
+}
 
 // half exchange of two complex registers across lane bit 5 (vdst = a: lanes
 // 32-63 of a <-> lanes 0-31 of b) / lane bit 4 (odd rows of a <-> even rows of b).

@@ -234,9 +234,11 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out,
 bool tdoa_gcc_phat_needs_split(int M, int N);
 // config-2 GCC-PHAT kernel (tdoa_phat1024.hip): host-built LDS table image
 // from the twiddles ([N] e^{-2 pi i k/N} then [N+1] e^{-2 pi i k/2N}),
-// Q15 window, lag prior and distinct lag tuples; empty if the shape differs
+// Q15 window, lag prior and distinct lag tuples with their first cells; empty
+// if the shape differs
 void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
-                         const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img);
+                         const float *prior, const uint32_t *tuples, const int32_t *tuple_cell,
+                         std::vector<uint8_t> &img);
 // the one-frame-per-wave config-2 kernel (tdoa_p1k_w64.hip): its image
 void tdoa_p1k_w64_image(int M, int N, int K, int U, const int32_t *win, const float *prior,
                         const uint32_t *tuples, std::vector<uint8_t> &img);

@@ -36,9 +36,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <type_traits>
+#include <vector>
 
 #include "tdoa_cplx.h"
 #include "tdoa_internal.h"
@@ -51,7 +55,7 @@ constexpr int P1K_ROW = 264;              // tile row stride, bytes (32 complex 
 constexpr int P1K_TILE = 32 * P1K_ROW;    // 8448 B: one transpose of one half-wave
 constexpr int P1K_KPAD = 128;             // lag slots per pair in the grid score table
 constexpr int P1K_WAVE_LDS = 2 * P1K_TILE;  // a wave's two transpose tiles (one per half-wave)
-constexpr int P1K_GB = 8;                 // grid tuples per lane per batch
+[[maybe_unused]] constexpr int P1K_GB = 8;               // grid tuples per lane per batch
 // LDS table image: twm [32][32] f2 | tw2 [16][32] f2 | win [512] f2 | prior [128] | tuples
 constexpr int P1K_IMG_FIXED = 32 * 32 * 8 + 16 * 32 * 8 + 512 * 8 + 128 * 4;
 
@@ -170,11 +174,34 @@ __device__ __forceinline__ f2 lds_f2(const char *base, int off)
     return *reinterpret_cast<const f2 *>(base + off);
 #endif
 }
+// the grid over tuples grouped by their first two lags (see the grid solve;
+// A/B variant, not the default: 25 % fewer LDS instructions per wave, but the
+// phase is latency-bound and the group's cell resolution adds ~1.9 k cycles,
+// 31.0 vs 30.4 us per 4096 frames -- DESIGN.md "Measured negative results")
+#ifndef P1K_GROUPS
+#define P1K_GROUPS 0
+#endif
+// the winner's first cell from LDS (tuple words carry it; see the grid end).
+// A/B variant, not the default: neutral (30.3 vs 30.35 us per 4096 frames) once
+// the lag / gate stores moved behind the grid, and it needs every 32-tuple row
+// to span < 2048 cells
+#ifndef P1K_CELL_LDS
+#define P1K_CELL_LDS 0
+#endif
+// the frame's lag / gate stores after the grid (see store_frame)
+#ifndef P1K_LATE_STORES
+#define P1K_LATE_STORES 1
+#endif
 // plain LDS read (the grid's gathers: data-dependent addresses, never merged,
 // and free to be scheduled around the other reads of the software pipeline)
 __device__ __forceinline__ f2 lds_f2_plain(const char *base, int off)
 {
     return *reinterpret_cast<const f2 *>(base + off);
+}
+// LDS read at a 32-bit LDS byte address
+__device__ __forceinline__ f2 lds_at(uint32_t addr)
+{
+    return *(const __attribute__((address_space(3))) f2 *)(uintptr_t)addr;
 }
 __device__ __forceinline__ void sts_f2(char *base, int off, f2 v)
 {
@@ -496,7 +523,9 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
 
     const int K = kp.K, S = kp.S;
     const bool do_grid = out.cell || out.xy || out.max_Lf;
+#if !P1K_GROUPS
     const int Upad = (kp.U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
+#endif
 
     auto fetch = [&](uint32_t(&w)[16], int64_t fr, int m) {
         const uint32_t *row = reinterpret_cast<const uint32_t *>(
@@ -583,8 +612,10 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                             wr[ck[c]] = wv[p][c];
                     }
             }
+#if !P1K_LATE_STORES
             if (ff < B && (ft & 31) == 0)
                 out.lags[ff * P + p] = bk - S;
+#endif
         };
 
         f2 U0[33], U1[33], y0, y31;
@@ -633,17 +664,40 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         finish_pair(2, y0, y31);
         LEAN_MARK();
         balance();
-        if (live && L.lane == 0 && out.gate)
-            out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
-
-        if (!do_grid)
+        // the frame's lags and gate (sample_compute.h:124-134): stored last
+        // unless P1K_LATE_STORES=0.  gfx9's vmcnt counts stores too, and the
+        // grid's one global load (the winner's first cell) waits in issue
+        // order: behind these stores it waited for their HBM write acks
+        auto store_frame = [&]() {
+            if (live && L.lane == 0) {
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    out.lags[f * P + p] = best[p];
+                if (out.gate)
+                    out.gate[f] = best[0] * best[0] + best[1] * best[1] + best[2] * best[2] > 4 ? 1 : 0;
+            }
+        };
+#if !P1K_LATE_STORES
+        store_frame();
+#endif
+        if (!do_grid) {
+#if P1K_LATE_STORES
+            store_frame();
+#endif
             return;
+        }
         // ---- grid solve (vga_heatmap.h:99-108) of the wave's two frames:
         // weighted scores [p][KPAD] f2 (frame hw in component hw) in the wave's
         // tile space, lanes split the distinct lag tuples (4 consecutive per
         // lane and step, ascending: a strict '>' keeps the first maximum)
         wave_lds_sync();  // after the last pair's row reads of these tiles
+#if P1K_CELL_LDS && !P1K_GROUPS
+        // [P][KPAD][2], 1 KiB-aligned in the wave's tiles: a gather address is
+        // then one and-or of a tuple field with the table base
+        float *wsc = (float *)(((uintptr_t)wtiles + 1023) & ~(uintptr_t)1023);
+#else
         float *wsc = (float *)wtiles;  // [P][KPAD][2]
+#endif
         const int gres = lane_res_sel(fresh_tid() & 31);
         const int gla = 2 * gres, glb = 2 * gres - 64;
         const int ck[4] = {glb + S, glb + 1 + S, gla + S, gla + 1 + S};
@@ -661,6 +715,194 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         }
         wave_lds_sync();  // the gathers read other lanes' score slots
         LEAN_MARK();
+#if P1K_GROUPS
+        // Tuples grouped by their first two lags (tdoa_phat1024_image): a
+        // group word holds the LDS offsets of lags l0, l1 and the first of n
+        // consecutive l2 (n = 3, 2, 1 by bucket), so a group costs 2 + n score
+        // gathers for its n tuples instead of 3 n, and (w0 + w1) is formed once
+        // -- the same association as ((w0 + w1) + w2), so the same floats.
+        // A lane keeps per frame the largest group maximum and its slot (strict
+        // '>', one compare per group instead of per tuple) and flags a tie with
+        // its running maximum.  At the end each lane re-reads its best group
+        // and takes the smallest first cell among the members equal to the
+        // maximum; the wave reduces (L, cell) -- the smallest cell among maxima
+        // is the first tuple (tuples are in first-cell order).  A lane whose
+        // maximum tied another of its groups rescans everything (rare: flat or
+        // equal scores).  Bucket sizes and tuple 0's cell: the image header,
+        // read as scalars from the global image.
+        const int *ghdr = reinterpret_cast<const int *>(static_cast<const char *>(kp.p1k_img) + P1K_IMG_FIXED);
+        const int gn3 = ghdr[0], gn2 = ghdr[1], gn1 = ghdr[2], gcell0 = ghdr[3];
+        const uint32_t *gw = tups + 4;
+        const uint16_t *gcl = reinterpret_cast<const uint16_t *>(gw + gn3 + gn2 + gn1);
+        const int gcb2 = 3 * gn3, gcb1 = gcb2 + 2 * gn2, gend = gn3 + gn2 + gn1;
+        // per frame: the largest group maximum, the first slot that reached it
+        // (strict '>') and the last slot that matched it ('>='); they differ
+        // exactly when a later group tied the maximum
+        float gv[2] = {-INFINITY, -INFINITY};
+        int gs[2] = {0, 0}, gsl[2] = {0, 0};
+        const char *ws = (const char *)wsc;
+        constexpr int R1 = P1K_KPAD * 8, R2 = 2 * P1K_KPAD * 8;
+        // volatile LDS reads: issued in program order, so the pipeline below is
+        // the one the hardware sees (the scheduler otherwise sank each step's
+        // word read to just before its gathers, and waited on it there)
+        auto gat = [&](auto nm, uint32_t w, f2 &a, f2 &b, f2 (&c)[decltype(nm)::value]) {
+            a = lds_rd(reinterpret_cast<const f2 *>(ws + (w & 0x3FFu)));
+            b = lds_rd(reinterpret_cast<const f2 *>(ws + R1 + ((w >> 10) & 0x3FFu)));
+#pragma unroll
+            for (int j = 0; j < decltype(nm)::value; j++)
+                c[j] = lds_rd(reinterpret_cast<const f2 *>(ws + R2 + (w >> 20) + 8 * j));
+        };
+        // one bucket of groups of NM tuples: slots [s0, s1), an even number of
+        // 64-slot rows, taken two rows (a unit) at a time.  Software-pipelined
+        // over two register sets (no copies, which would wait for the loads):
+        // while unit u is compared, unit u+1's 2 (2 + NM) gathers are in flight,
+        // and every word is read before the gathers issued ahead of its own, so
+        // that waiting for it (LDS returns in order) never waits for those
+        auto bucket = [&](auto nm, int s0, int s1) {
+            constexpr int NM = decltype(nm)::value;
+            if (s0 >= s1)
+                return;
+            const int last = s1 - 64;  // (clamped units past the end: harmless re-reads)
+            const int nu = (s1 - s0) / 128;
+            auto words = [&](uint32_t (&w)[2], int u) {
+                w[0] = lds_rd_u32(gw + imin(s0 + 128 * u, last) + lane64);
+                w[1] = lds_rd_u32(gw + imin(s0 + 128 * u + 64, last) + lane64);
+            };
+            auto gather = [&](const uint32_t (&w)[2], f2 (&a)[2], f2 (&b)[2], f2 (&c)[2][NM]) {
+                gat(nm, w[0], a[0], b[0], c[0]);
+                gat(nm, w[1], a[1], b[1], c[1]);
+            };
+            auto consume = [&](const f2 (&a)[2], const f2 (&b)[2], const f2 (&c)[2][NM], int u) {
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    const f2 part = a[r] + b[r];
+                    f2 L[NM];
+#pragma unroll
+                    for (int j = 0; j < NM; j++)
+                        L[j] = part + c[r][j];
+                    float m[2] = {L[0].x, L[0].y};
+#pragma unroll
+                    for (int j = 1; j < NM; j++) {
+                        m[0] = fmaxf(m[0], L[j].x);
+                        m[1] = fmaxf(m[1], L[j].y);
+                    }
+                    const int sl = s0 + 128 * u + 64 * r + lane64;
+#pragma unroll
+                    for (int f = 0; f < 2; f++) {
+                        const bool gt = m[f] > gv[f];
+                        gsl[f] = m[f] >= gv[f] ? sl : gsl[f];
+                        gs[f] = gt ? sl : gs[f];
+                        gv[f] = gt ? m[f] : gv[f];
+                    }
+                }
+            };
+            f2 a0[2], b0[2], c0[2][NM], a1[2], b1[2], c1[2][NM];
+            uint32_t w2[2], w3[2];
+            // (the prologue leaves the loads in the loop's own order -- unit 0,
+            // then the words of unit 2, then unit 1 -- so the wait counts at the
+            // loop head are the steady state's, not a full drain)
+            words(w2, 0);
+            gather(w2, a0, b0, c0);
+            words(w3, 1);
+            words(w2, 2);
+            gather(w3, a1, b1, c1);
+            // whole pairs of units whose loads stay inside the bucket, in a
+            // branch-free body (a branch inside made the wait-count pass drain
+            // every load at the loop head; scheduling barriers: the scheduler
+            // hoisted unit u+1's sums above unit u+2's gathers, the same drain)
+            int u = 0;
+            for (; u + 3 < nu; u += 2) {
+                consume(a0, b0, c0, u);
+                words(w3, u + 3);
+                gather(w2, a0, b0, c0);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(a1, b1, c1, u + 1);
+                words(w2, u + 4);
+                gather(w3, a1, b1, c1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // the last one to three units, none loaded past the end
+            consume(a0, b0, c0, u);
+            if (u + 2 < nu)
+                gather(w2, a0, b0, c0);
+            if (u + 1 < nu)
+                consume(a1, b1, c1, u + 1);
+            if (u + 2 < nu)
+                consume(a0, b0, c0, u + 2);
+        };
+        bucket(std::integral_constant<int, 3>{}, 0, gn3);
+        bucket(std::integral_constant<int, 2>{}, gn3, gn3 + gn2);
+        bucket(std::integral_constant<int, 1>{}, gn3 + gn2, gend);
+        LEAN_MARK();
+        // smallest first cell among the members of group slot sl whose L (frame
+        // f) equals v; INT_MAX if none (the rare full rescan)
+        auto group_cell = [&](int sl, int f, float v) {
+            const int nm = sl < gn3 ? 3 : (sl < gn3 + gn2 ? 2 : 1);
+            const int cb = sl < gn3 ? 3 * sl : (sl < gn3 + gn2 ? gcb2 + 2 * (sl - gn3) : gcb1 + (sl - gn3 - gn2));
+            const uint32_t w = gw[sl];
+            const f2 part = lds_f2_plain(ws, (int)(w & 0x3FFu)) + lds_f2_plain(ws, R1 + (int)((w >> 10) & 0x3FFu));
+            int mc = INT_MAX;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                if (j < nm) {
+                    const f2 Lg = part + lds_f2_plain(ws, R2 + (int)(w >> 20) + 8 * j);
+                    if ((f ? Lg.y : Lg.x) == v)
+                        mc = imin(mc, (int)gcl[cb + j]);
+                }
+            }
+            return mc;
+        };
+        // each lane's candidate per frame: its best group's members equal to
+        // the maximum, both frames' words and cells read together, then the
+        // gathers (two LDS round trips)
+        int cand[2];
+        {
+            uint32_t bw[2];
+            int bnm[2], bc[2][3];
+#pragma unroll
+            for (int f = 0; f < 2; f++) {
+                const int sl = gs[f];
+                bnm[f] = sl < gn3 ? 3 : (sl < gn3 + gn2 ? 2 : 1);
+                const int cb = sl < gn3 ? 3 * sl : (sl < gn3 + gn2 ? gcb2 + 2 * (sl - gn3) : gcb1 + (sl - gn3 - gn2));
+                bw[f] = gw[sl];
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    bc[f][j] = gcl[cb + imin(j, bnm[f] - 1)];
+            }
+#pragma unroll
+            for (int f = 0; f < 2; f++) {
+                const uint32_t w = bw[f];
+                const f2 part = lds_f2_plain(ws, (int)(w & 0x3FFu)) + lds_f2_plain(ws, R1 + (int)((w >> 10) & 0x3FFu));
+                int mc = INT_MAX;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const f2 Lg = part + lds_f2_plain(ws, R2 + (int)(w >> 20) + 8 * j);
+                    if (j < bnm[f] && (f ? Lg.y : Lg.x) == gv[f])
+                        mc = imin(mc, bc[f][j]);
+                }
+                cand[f] = gv[f] > -INFINITY ? mc : INT_MAX;
+            }
+        }
+        int wcell[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            int ci = cand[j];
+            int gk = fkey(gv[j]);
+            wave_argmax_key(gk, ci);
+            const float V = fkey_value(gk);
+            if (__ballot(gsl[j] != gs[j] && gv[j] == V && V > -INFINITY)) {
+                // rare: some lane's maximum tied another of its groups -- the
+                // smallest first cell of every member whose L equals it
+                int mc = INT_MAX;
+                for (int sl = lane64; sl < gend; sl += 64)
+                    mc = imin(mc, group_cell(sl, j, V));
+                ci = wave_reduce<false>(mc);
+            }
+            wcell[j] = ci == INT_MAX ? gcell0 : ci;  // no maximum (NaN scores): tuple 0
+            gv[j] = V;
+        }
+        LEAN_MARK();
+#else
         float gv[2] = {-INFINITY, -INFINITY};
         int gu[2] = {INT_MAX, INT_MAX};
         const char *ws = (const char *)wsc;
@@ -670,13 +912,26 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         // Software-pipelined by one step: the next step's tuple words and 12
         // gathers are in flight while this step's sums and compares run (the
         // loop is bound by LDS latency, not by its few VALU operations).
+#if P1K_CELL_LDS
+        const uint32_t wsb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)ws;
+#endif
         auto gather = [&](const uint32_t (&qq)[4], f2 (&g)[4][3]) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
+#if P1K_CELL_LDS
+                // tuple fields: the lag slots' byte offsets (slot << 3) in bits
+                // 3-9, 10-16 (>> 7), 17-23 (>> 14); the 1 KiB-aligned base
+                // goes in by an or.  The first cell's offset from its row's
+                // is in bits 24-31 and 0-2
+                g[i][0] = lds_at((qq[i] & 0x3F8u) | wsb);
+                g[i][1] = lds_at((((qq[i] >> 7) & 0x3F8u) | wsb) + P1K_KPAD * 8);
+                g[i][2] = lds_at((((qq[i] >> 14) & 0x3F8u) | wsb) + 2 * P1K_KPAD * 8);
+#else
                 // tuple fields are byte offsets of f2 slots in [p][KPAD]
                 g[i][0] = lds_f2_plain(ws, (int)(qq[i] & 0x3FFu));
                 g[i][1] = lds_f2_plain(ws, P1K_KPAD * 8 + (int)((qq[i] >> 10) & 0x3FFu));
                 g[i][2] = lds_f2_plain(ws, 2 * P1K_KPAD * 8 + (int)(qq[i] >> 20));
+#endif
             }
         };
         uint32_t q[4];
@@ -718,15 +973,30 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             consume(gn, u0 + 256);
         }
         LEAN_MARK();
-        // each lane requests the first cell of its own candidate before the
+        // each lane looks up the first cell of its own candidate before the
         // wave reduction: the winner's comes back by a lane read, not by a
         // dependent load after it
         int mycell[2], myu[2];
+#if P1K_CELL_LDS
+        // from LDS: the tuple word's cell offset plus its 32-tuple row's first
+        // cell (two LDS reads).  No global load may be pending here: gfx9's
+        // vmcnt counts stores too, and every wait for such a load behind the
+        // outputs below waited for their HBM write acks (~2.5 k cycles)
+        const int *rowcell = reinterpret_cast<const int *>(tups + Upad);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            myu[j] = gu[j];
+            const int uc = (gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j];
+            const uint32_t tw = tups[uc];
+            mycell[j] = rowcell[uc >> 5] + (int)((tw >> 24) | ((tw & 7u) << 8));
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             myu[j] = gu[j];
             mycell[j] = kp.tuple_cell[(gu[j] < 0 || gu[j] >= kp.U) ? 0 : gu[j]];
         }
+#endif
         // (max L, first tuple) over the wave by keys (gv is -inf, never NaN,
         // where a lane had no L above it: those lanes keep gu = INT_MAX)
         int gk[2];
@@ -738,12 +1008,18 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         }
         LEAN_MARK();
         int wcell[2];
+#if P1K_CELL_LDS
+        const int tuple_cell0 = rowcell[0];  // (offset 0)
+#else
+        const int tuple_cell0 = kp.tuple_cell[0];
+#endif
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int fu = gu[j];
             const uint64_t wm = __ballot(myu[j] == fu && fu >= 0 && fu < kp.U);
-            wcell[j] = wm ? __builtin_amdgcn_readlane(mycell[j], __builtin_ctzll(wm)) : kp.tuple_cell[0];
+            wcell[j] = wm ? __builtin_amdgcn_readlane(mycell[j], __builtin_ctzll(wm)) : tuple_cell0;
         }
+#endif
         if (lane64 == 63) {
             const int cells[2] = {wcell[0], wcell[1]};  // no winner (NaN scores): tuple 0
 #pragma unroll
@@ -762,6 +1038,9 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
                 }
             }
         }
+#if P1K_LATE_STORES
+        store_frame();
+#endif
         LEAN_MARK();
     }
 #ifdef TDOA_DIAG
@@ -790,22 +1069,63 @@ extern "C" int tdoa_diag_fetch_p1k(unsigned long long *host, int n)
 namespace {
 constexpr int P1K_NW = 8;  // waves per workgroup (two per SIMD)
 
-constexpr size_t p1k_lds(int U)
-{
-    return (size_t)P1K_NW * P1K_WAVE_LDS + P1K_IMG_FIXED +
-           (size_t)(U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64) * 4;
-}
+// dynamic LDS of a launch: the waves' tiles and the whole table image
+constexpr size_t p1k_lds(int img_bytes) { return (size_t)P1K_NW * P1K_WAVE_LDS + (size_t)img_bytes; }
 }  // namespace
 
 // LDS table image of k_phat1024 (layout of the kernel's shared memory from twm on)
 void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int32_t *win,
-                         const float *prior, const uint32_t *tuples, std::vector<uint8_t> &img)
+                         const float *prior, const uint32_t *tuples, const int32_t *tuple_cell,
+                         std::vector<uint8_t> &img)
 {
     img.clear();
     if (M != 3 || N != 1024 || K > P1K_KPAD - 1)
         return;
+#if P1K_GROUPS
+    // groups: tuples of equal (l0, l1) whose l2 are consecutive, at most 3 per
+    // group (config 2: 1121 groups of 3 / 2 / 1 for 2469 tuples), bucketed by
+    // size, each bucket in the order of its groups' first tuples (neighbouring
+    // lanes, neighbouring cells and lag slots) and padded to whole waves
+    struct Grp {
+        int l0, l1, l2, n, u0;
+        int cell[3];
+    };
+    std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> by;  // (l0, l1) -> (l2, u)
+    for (int u = 0; u < U; u++)
+        by[{(int)(tuples[u] & 0xFFu), (int)((tuples[u] >> 8) & 0xFFu)}].push_back({(int)((tuples[u] >> 16) & 0xFFu), u});
+    std::vector<Grp> bk[4];
+    for (auto &kv : by) {
+        auto &v = kv.second;
+        std::sort(v.begin(), v.end());
+        for (size_t i = 0; i < v.size();) {
+            Grp g{kv.first.first, kv.first.second, v[i].first, 0, INT_MAX, {0, 0, 0}};
+            while (i < v.size() && g.n < 3 && v[i].first == g.l2 + g.n) {
+                if (tuple_cell[v[i].second] < 0 || tuple_cell[v[i].second] >= 0xFFFF)
+                    return;  // cells are 16-bit in the table
+                g.cell[g.n++] = tuple_cell[v[i].second];
+                g.u0 = std::min(g.u0, v[i].second);
+                i++;
+            }
+            bk[g.n].push_back(g);
+        }
+    }
+    int nslot[4];
+    for (int n = 1; n <= 3; n++) {
+        std::sort(bk[n].begin(), bk[n].end(), [](const Grp &x, const Grp &y) { return x.u0 < y.u0; });
+        nslot[n] = ((int)bk[n].size() + 127) / 128 * 128;  // whole pairs of 64-slot steps
+    }
+    const int ncell = 3 * nslot[3] + 2 * nslot[2] + nslot[1];
+    const size_t bytes = (size_t)P1K_IMG_FIXED + 16 + 4 * (size_t)(nslot[3] + nslot[2] + nslot[1]) + 2 * (size_t)ncell;
+    img.resize((bytes + 15) / 16 * 16);
+#else
     const int Upad = (U + P1K_GB * 64 - 1) / (P1K_GB * 64) * (P1K_GB * 64);
+#if P1K_CELL_LDS
+    img.resize((size_t)P1K_IMG_FIXED + (size_t)Upad * 4 + (size_t)(Upad / 32) * 4);  // + the row cells
+#else
+    (void)tuple_cell;
     img.resize((size_t)P1K_IMG_FIXED + (size_t)Upad * 4);
+#endif
+#endif
     float *f = (float *)img.data();
     const float *tw2 = tw + 2 * N;
     for (int k = 0; k < 32; k++)  // twm [k][r] = W_1024^{r k}
@@ -831,12 +1151,56 @@ void tdoa_phat1024_image(int M, int N, int K, int U, const float *tw, const int3
     for (int k = 0; k < 128; k++)
         f[k] = k < K ? prior[k] : 0.0f;
     uint32_t *t = (uint32_t *)(f + 128);
+#if P1K_GROUPS
+    // header: slots per bucket (n = 3, 2, 1), tuple 0's cell; then the group
+    // words (LDS byte offsets of l0, l1 and the first l2 in a wave's [p][KPAD]
+    // f2 score table, 10 bits each; padding groups start at slot 127 of every
+    // pair, -inf) and the member cells (u16, bucket n: [slot][n])
+    int32_t *hdr = (int32_t *)t;
+    hdr[0] = nslot[3];
+    hdr[1] = nslot[2];
+    hdr[2] = nslot[1];
+    hdr[3] = U > 0 ? tuple_cell[0] : 0;
+    t += 4;
+    uint16_t *cl = (uint16_t *)(t + nslot[3] + nslot[2] + nslot[1]);
+    for (int n = 3; n >= 1; n--) {
+        for (int e = 0; e < nslot[n]; e++) {
+            const bool real = e < (int)bk[n].size();
+            const Grp g = real ? bk[n][e] : Grp{127, 127, 128 - n, n, 0, {0xFFFF, 0xFFFF, 0xFFFF}};
+            *t++ = ((uint32_t)g.l0 << 3) | ((uint32_t)g.l1 << 13) | ((uint32_t)g.l2 << 23);
+            for (int j = 0; j < n; j++)
+                *cl++ = (uint16_t)g.cell[j];
+        }
+    }
+#else
     // tuples as LDS byte offsets into a wave's [p][KPAD] f2 score table, 10 bits
     // per pair; padding tuple (127, 127, 127) scores -inf
+#if P1K_CELL_LDS
+    // (lag slots 7 bits each, then the first cell minus its 32-tuple row's
+    // first cell in 11 bits; a table with a row that spans more has no image:
+    // the generic kernel runs it)
+    int32_t *rowcell = (int32_t *)(t + Upad);
+    for (int r = 0; r < Upad / 32; r++) {
+        const int e0 = 32 * r, e1 = std::min(U, e0 + 32) - 1;
+        rowcell[r] = e0 >= U ? 0 : tuple_cell[e0];
+        if (e0 < U && tuple_cell[e1] - tuple_cell[e0] >= 2048) {
+            img.clear();
+            return;
+        }
+    }
+    for (int e = 0; e < Upad; e++) {
+        const uint32_t wd = e < U ? tuples[e] : 0x007F7F7Fu;
+        const uint32_t dc = e < U ? (uint32_t)(tuple_cell[e] - rowcell[e >> 5]) : 0u;
+        t[e] = ((wd & 0x7Fu) << 3) | (((wd >> 8) & 0x7Fu) << 10) | (((wd >> 16) & 0x7Fu) << 17) |
+               ((dc & 0xFFu) << 24) | (dc >> 8);
+    }
+#else
     for (int e = 0; e < Upad; e++) {
         const uint32_t wd = e < U ? tuples[e] : 0x007F7F7Fu;
         t[e] = ((wd & 0xFFu) << 3) | (((wd >> 8) & 0xFFu) << 13) | (((wd >> 16) & 0xFFu) << 23);
     }
+#endif
+#endif
 }
 
 // config-2 shape (M = 3, N = 1024, S <= 63) with a tuple table that fits the tail
@@ -846,7 +1210,8 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp)
         return false;
     // grid scores of a wave's two frames live in its tiles: [3][KPAD] float2 = 3 KiB
     static_assert(3 * P1K_KPAD * 8 <= P1K_WAVE_LDS, "grid scores exceed the wave's tiles");
-    return p1k_lds(kp.U) + 64 <= 160 * 1024;  // + the static progress words
+    // the image loads as at most 4 units of 16 B per thread (k_p1k_lean's staging)
+    return kp.p1k_img_bytes <= 4 * P1K_NW * 64 * 16 && p1k_lds(kp.p1k_img_bytes) + 64 <= 160 * 1024;  // + the static progress words
 }
 
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
@@ -864,7 +1229,7 @@ int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int
     const int64_t grid = (B + NF - 1) / NF;
     if (grid > 0x7FFFFFFF)
         return tdoa_set_error(-1, "k_p1k_lean: batch too large for one launch");
-    hipLaunchKernelGGL(k_p1k_lean, dim3((unsigned)grid), dim3(P1K_NW * 64), p1k_lds(kp.U), (hipStream_t)stream,
+    hipLaunchKernelGGL(k_p1k_lean, dim3((unsigned)grid), dim3(P1K_NW * 64), p1k_lds(kp.p1k_img_bytes), (hipStream_t)stream,
                        kp, out, frames, B, e2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

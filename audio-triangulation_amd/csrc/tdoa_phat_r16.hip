@@ -68,11 +68,6 @@ constexpr bool f16_win_lds()
 {
     return C == 4096;
 }
-__device__ __forceinline__ uint32_t lds_rd_u32(const uint32_t *p)
-{
-    typedef __attribute__((address_space(3))) uint32_t lds_u32;
-    return *(const volatile lds_u32 *)(const lds_u32 *)p;
-}
 #if F16_VLDS
 #define F16_LD(p) lds_rd(p)
 #else
