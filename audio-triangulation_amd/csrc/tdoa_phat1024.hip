@@ -498,7 +498,10 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
     __builtin_amdgcn_s_setprio(2);
     int phase = 0;
     auto balance = [&]() {
-        volatile int *pv = prog;
+        // through an LDS-address-space pointer: ds_write / ds_read.  A generic
+        // volatile pointer made them flat accesses, and the flat load's wait
+        // (vmcnt(0) lgkmcnt(0)) also waited for the next mic's words in flight
+        volatile __attribute__((address_space(3))) int *pv = (volatile __attribute__((address_space(3))) int *)prog;
         ++phase;
         if (lane64 == 0)
             pv[wave] = phase;

@@ -642,10 +642,14 @@ constexpr size_t frame16_lds_base()
 // per frame (the least-squares lags) stay where they are used instead of being
 // hoisted out of the frame loop and held in scalar registers across the
 // transforms.  kp and out are the kernel's first two arguments (kernarg
-// offsets 0 and sizeof(kp) rounded to 8).
-__device__ __forceinline__ const char *kernarg_base()
+// offsets 0 and sizeof(kp) rounded to 8).  The pointer keeps the constant
+// address space: its loads are scalar (s_load, lgkmcnt only).  A generic
+// pointer made them flat loads, whose vmcnt wait also waited for the next
+// frame's prefetched words.
+typedef __attribute__((address_space(4))) const char kchar;
+__device__ __forceinline__ kchar *kernarg_base()
 {
-    const char *k = (const char *)__builtin_amdgcn_kernarg_segment_ptr();
+    kchar *k = (kchar *)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(k));
     return k;
 }
@@ -653,9 +657,10 @@ __device__ __forceinline__ const char *kernarg_base()
 // (kp, out) stay k_frame16's first two parameters.
 static_assert(alignof(tdoa_kparams) <= 8 && alignof(tdoa_kout) == 8,
               "kernarg_out(): tdoa_kout must sit at sizeof(tdoa_kparams) rounded to 8");
-__device__ __forceinline__ const tdoa_kout *kernarg_out()
+__device__ __forceinline__ const __attribute__((address_space(4))) tdoa_kout *kernarg_out()
 {
-    return reinterpret_cast<const tdoa_kout *>(kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
+    return reinterpret_cast<const __attribute__((address_space(4))) tdoa_kout *>(
+        kernarg_base() + ((sizeof(tdoa_kparams) + 7) & ~(size_t)7));
 }
 
 // The outputs of NP pairs from one wave (NP = 2: two independent argmax
