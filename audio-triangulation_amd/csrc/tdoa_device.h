@@ -67,9 +67,11 @@ __device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, const RingSl
         // loads (7 aligned dwords), shifted to the sample's byte, then every
         // third byte (eight byte loads per chunk bound the staging on the
         // texture units)
-        const uintptr_t a = (uintptr_t)(cap + j * 3);
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(a & 3u);
+        // (the word pointer by pointer arithmetic: an integer-to-pointer cast
+        // loses the global address space, and flat loads' waits drain LDS too)
+        const uint8_t *ab = cap + j * 3;
+        const uint32_t sh = (uint32_t)((uintptr_t)ab & 3u);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(ab - sh);
         uint32_t w[7];
 #pragma unroll
         for (int d = 0; d < 7; d++)

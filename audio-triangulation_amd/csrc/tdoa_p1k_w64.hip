@@ -98,6 +98,9 @@ __host__ __device__ constexpr int w64_coli(int l) { return (l >> 2) + 16 * (l & 
 __device__ __forceinline__ f2 lds_f2(const char *base, int off) { return *reinterpret_cast<const f2 *>(base + off); }
 __device__ __forceinline__ void sts_f2(char *base, int off, f2 v) { *reinterpret_cast<f2 *>(base + off) = v; }
 __device__ __forceinline__ void pin(f2 &x) { asm volatile("" : "+v"(x)); }
+// volatile LDS words through an LDS-address-space pointer (ds_read / ds_write;
+// a generic volatile pointer gives flat accesses, whose waits drain vmcnt too)
+typedef volatile __attribute__((address_space(3))) int vlds_int;
 typedef short v2s_t __attribute__((ext_vector_type(2)));
 
 // the lane id through an opaque move: lane-dependent values derived from it
@@ -257,7 +260,7 @@ struct W64Lane {
 // than the slowest wave of its SIMD drops to the low priority until it catches up
 __device__ __forceinline__ void w64_balance(const W64Lane &W)
 {
-    volatile int *pv = W.prog;
+    vlds_int *pv = (vlds_int *)W.prog;
     const int ph = ++W.phase;
     if ((W.L8 >> 3) == 0)
         pv[W.pslot] = ph;
@@ -706,10 +709,10 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
         // fence); the odd wave writes only after the even wave has finished
         // reading its tile.
         const int odd = wave & 1;
-        volatile int *flag = prog + W64_NW + (wave & ~1);  // [pair][2]: 1 table half written, 2 partials
+        vlds_int *flag = (vlds_int *)(prog + W64_NW + (wave & ~1));  // [pair][2]: 1 table half written, 2 partials
         const int toff = (W64_TILES + __builtin_amdgcn_readfirstlane(wave & ~1) * W64_TILE + 1023) & ~1023;
         float *wsc = (float *)(smem + toff);  // [p][KPAD][2]
-        auto wait_flag = [&](volatile int *fp, int v) {
+        auto wait_flag = [&](vlds_int *fp, int v) {
             while (__builtin_amdgcn_readfirstlane(*fp) < v)
                 __builtin_amdgcn_s_sleep(1);
         };
@@ -810,7 +813,7 @@ __global__ void __launch_bounds__(1024) k_p1k_w64(tdoa_kparams kp, tdoa_kout out
         if (lane == 0)
             flag[odd] = 2;
         wait_flag(flag + (odd ^ 1), 2);
-        const volatile int *px = prog + 2 * W64_NW + 4 * (wave ^ 1);
+        const vlds_int *px = (const vlds_int *)(prog + 2 * W64_NW + 4 * (wave ^ 1));
         const int ok_ = __builtin_amdgcn_readfirstlane(px[0]), oi = __builtin_amdgcn_readfirstlane(px[1]),
                   oc = __builtin_amdgcn_readfirstlane(px[2]);
         int mk = fkey(mv[odd]), mi = gu[odd], cell = cell2[odd];

@@ -265,9 +265,11 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
         const uint8_t *cap = sp.capture + (size_t)st * cl * M;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
-            const uintptr_t p = (uintptr_t)(cap + (size_t)(fast[r] ? jr[r] : 0) * M);
-            const uint32_t *wp = reinterpret_cast<const uint32_t *>(p & ~(uintptr_t)3);
-            sh[r] = (uint32_t)(p & 3u);
+            // (pointer arithmetic, not an integer-to-pointer cast: that made
+            // these flat loads, whose waits also drain the LDS counter)
+            const uint8_t *pb = cap + (size_t)(fast[r] ? jr[r] : 0) * M;
+            sh[r] = (uint32_t)((uintptr_t)pb & 3u);
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(pb - sh[r]);
 #pragma unroll
             for (int k = 0; k <= CW; k++)
                 w[r][k] = fast[r] ? wp[k] : 0u;
