@@ -188,6 +188,17 @@ __device__ __forceinline__ f2 lds_f2(const char *base, int off)
 #ifndef P1K_CELL_LDS
 #define P1K_CELL_LDS 0
 #endif
+// the SIMD issue balance (s_setprio by phase progress; see the kernel).
+// Without it (P1K_BALANCE=0): 31.8 vs 29.1 us per 4096 frames
+#ifndef P1K_BALANCE
+#define P1K_BALANCE 1
+#endif
+// mic 2's words requested inside mic 1's forward (as mic 1's inside mic 0's).
+// A/B variant, not the default: 29.9 vs 29.1 us (the column pass of pair
+// (0,1) then runs with 16 more live registers)
+#ifndef P1K_W2_EARLY
+#define P1K_W2_EARLY 0
+#endif
 // the frame's lag / gate stores after the grid (see store_frame)
 #ifndef P1K_LATE_STORES
 #define P1K_LATE_STORES 1
@@ -501,6 +512,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         // through an LDS-address-space pointer: ds_write / ds_read.  A generic
         // volatile pointer made them flat accesses, and the flat load's wait
         // (vmcnt(0) lgkmcnt(0)) also waited for the next mic's words in flight
+#if P1K_BALANCE
         volatile __attribute__((address_space(3))) int *pv = (volatile __attribute__((address_space(3))) int *)prog;
         ++phase;
         if (lane64 == 0)
@@ -510,6 +522,7 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
             __builtin_amdgcn_s_setprio(0);
         else
             __builtin_amdgcn_s_setprio(2);
+#endif
     };
     Lane L;
     L.hw = hw;
@@ -631,16 +644,25 @@ __global__ void __launch_bounds__(512, 2) k_p1k_lean(tdoa_kparams kp, tdoa_kout 
         });
         LEAN_MARK();
         balance();
+#if P1K_W2_EARLY
+        lean_forward(L, w1, U1, e2, [&] {
+            fetch(w2, f, 2);
+            balance();
+        });
+#else
         lean_forward(L, w1, U1, e2, [&] { balance(); });
+#endif
         LEAN_MARK();
         balance();
         {
             f2 v[32];
             lean_pretwiddle<true>(L, U0, U1, v);  // pair 0: (0, 1)
             fft_col_lds<true, false>(L, v, L.tileA);
+#if !P1K_W2_EARLY
             // mic 2's words: fetched after the pair's column pass, the kernel's
             // register peak (two unit spectra + a working column)
             fetch(w2, f, 2);
+#endif
             lean_row_inv(L, L.tileA, y0, y31);
         }
         finish_pair(0, y0, y31);

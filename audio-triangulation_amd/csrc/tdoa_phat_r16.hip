@@ -68,6 +68,17 @@ constexpr bool f16_win_lds()
 {
     return C == 4096;
 }
+// the other shapes (C = 2048: LDS is full with the deferred epilogue) keep the
+// thread's 8 window words in registers for the launch instead of reading them
+// from L2 at every frame's start (F16_WIN_REG=0: from L2)
+#ifndef F16_WIN_REG
+#define F16_WIN_REG 1
+#endif
+template <int C>
+constexpr int f16_win_mode()
+{
+    return f16_win_lds<C>() ? 1 : (F16_WIN_REG ? 2 : 0);
+}
 #if F16_VLDS
 #define F16_LD(p) lds_rd(p)
 #else
@@ -511,15 +522,20 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 // and three register passes in the group's LDS slot buf): the DC sum of the
 // group's words w, the Q15 window, radix R1 / 16 / 16 Stockham passes; Z[j + T q]
 // ends in buf at pidx(j + T q), after a closing barrier
-template <int C, bool WL, typename Mark>
-__device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, f2 *buf, int *red,
-                                                const f2 *tt, int tid, int g, int j, int pj, int log2N, Mark mark)
+// WM: where the thread's window words come from -- 0 global (L2), 1 LDS (win
+// is the LDS copy), 2 registers (wr, loaded once per launch)
+template <int C, int WM, typename Mark>
+__device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, const uint32_t (&wr)[8],
+                                                f2 *buf, int *red, const f2 *tt, int tid, int g, int j, int pj,
+                                                int log2N, Mark mark)
 {
     constexpr int T = C / 16, R1 = C / 256;
     uint32_t wn[8];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        if constexpr (WL)
+        if constexpr (WM == 2)
+            wn[s] = wr[s];
+        else if constexpr (WM == 1)
             wn[s] = lds_rd_u32(win + j + T * s);
         else
             wn[s] = win[j + T * s];
@@ -796,6 +812,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const f2 t = twC(reinterpret_cast<const f2 *>(kp.r16_tw), r, l < 32 ? l : 64 - l);
         tw3[threadIdx.x] = f2{t.x, l < 32 ? -t.y : t.y};
     }
+    uint32_t wr[8] = {};  // f16_win_mode 2: this thread's window words
+    if constexpr (f16_win_mode<C>() == 2) {
+        const int j0 = (int)threadIdx.x - g * T;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2++)
+            wr[s2] = win[j0 + T * s2];
+    }
     if constexpr (f16_win_lds<C>()) {
         for (int i = threadIdx.x; i < C / 2; i += 1024)
             winl[i] = win[i];
@@ -860,7 +883,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
-    frame16_forward<C, f16_win_lds<C>()>(w, f16_win_lds<C>() ? winl : win, buf, red, tt, tid, g, j, pj, kp.log2N,
+    frame16_forward<C, f16_win_mode<C>()>(w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N,
                                          [&] {
         if (fr == diag_fr)
             F16_MARK();  // the forward's barriers (diagnostic build)
@@ -1356,7 +1379,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16w(tdoa_kparams kp, tdoa_kout
 #endif
             F16W_MARK();
         }
-        frame16_forward<C, false>(w, win, buf, red, tt, tid, g, j, pj, kp.log2N, [] {});
+        const uint32_t wr0[8] = {};
+        frame16_forward<C, 0>(w, win, wr0, buf, red, tt, tid, g, j, pj, kp.log2N, [] {});
         if (fr == diag_fr)
             F16W_MARK();  // forward transforms done
         // ---- 2. split + unit normalisation: thread b reads Z_m[b], Z_m[C - b]
