@@ -63,10 +63,15 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 #endif
 // the Q15 window words of config 3's shape (C = 4096) sit in LDS (8 KiB):
 // read from L2 at every frame's start, their latency followed the DC barrier
+// C = 4096 too keeps its window words in registers (F16_WIN_LDS4096=1: the
+// LDS copy instead; config 3 3.70 vs 3.62 ms per step, same box)
+#ifndef F16_WIN_LDS4096
+#define F16_WIN_LDS4096 0
+#endif
 template <int C>
 constexpr bool f16_win_lds()
 {
-    return C == 4096;
+    return C == 4096 && F16_WIN_LDS4096;
 }
 // the other shapes (C = 2048: LDS is full with the deferred epilogue) keep the
 // thread's 8 window words in registers for the launch instead of reading them
