@@ -63,6 +63,14 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
 #endif
 // the Q15 window words of config 3's shape (C = 4096) sit in LDS (8 KiB):
 // read from L2 at every frame's start, their latency followed the DC barrier
+// the prefetched frame words waited for before the output stores (k_frame16)
+#ifndef F16_PIN
+#define F16_PIN 1
+#endif
+// the split's twiddles in registers for the launch (see k_frame16)
+#ifndef F16_TW_REG
+#define F16_TW_REG 1
+#endif
 // C = 4096 too keeps its window words in registers (F16_WIN_LDS4096=1: the
 // LDS copy instead; config 3 3.70 vs 3.62 ms per step, same box)
 #ifndef F16_WIN_LDS4096
@@ -817,6 +825,15 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const f2 t = twC(reinterpret_cast<const f2 *>(kp.r16_tw), r, l < 32 ? l : 64 - l);
         tw3[threadIdx.x] = f2{t.x, l < 32 ? -t.y : t.y};
     }
+#if F16_TW_REG
+    // W_2C^b of this thread's split bins and W_2C^{C/2}: loaded once for the
+    // launch (read per frame from L2, their latency opened every split)
+    f2 twb[NS];
+#pragma unroll
+    for (int s2 = 0; s2 < NS; s2++)
+        twb[s2] = tw2[(int)threadIdx.x + 1024 * s2];
+    f2 twh = tw2[C / 2];
+#endif
     uint32_t wr[8] = {};  // f16_win_mode 2: this thread's window words
     if constexpr (f16_win_mode<C>() == 2) {
         const int j0 = (int)threadIdx.x - g * T;
@@ -876,6 +893,32 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             w[s] = __builtin_nontemporal_load(x + T * s);
     };
     fetch(blockIdx.x);
+    // the next frame's words are waited for here, before this wave's output
+    // stores: gfx9's vmcnt counts stores and retires in order, and with stores
+    // in branches the loop head's wait for the words was vmcnt(0) -- it also
+    // waited for the frame's last stores to be acknowledged (F16_PIN=0: off)
+    auto pin_words = [&] {
+#if F16_PIN
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+            asm volatile("" : "+v"(w[s]));
+#endif
+    };
+#if F16_PIN
+    // and every value loaded before the loop is waited for before it: a load
+    // still pending on the loop's entry edge put a vmcnt(0) at the loop head,
+    // which on the back edge waited for the stores
+    pin_words();
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+        asm volatile("" : "+v"(wr[s]));
+#if F16_TW_REG
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+        asm volatile("" : "+v"(twb[s].x), "+v"(twb[s].y));
+    asm volatile("" : "+v"(twh.x), "+v"(twh.y));
+#endif
+#endif
     for (int64_t fr = blockIdx.x; fr < B; fr += gridDim.x) {
     // thread indices the compiler cannot prove loop-invariant: the passes'
     // twiddle reads stay in the body instead of being hoisted (and spilled)
@@ -901,11 +944,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // W_2C^b of this thread's bins (the split and every pair's pre-twiddle), W_2C^{C/2}
     // (requested before the forward's last pass instead, they measured slower:
     // 4.89 vs 4.71 ms per config-3 step)
+#if !F16_TW_REG
     f2 twb[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++)
         twb[s] = tw2[tid + 1024 * s];
     const f2 twh = tw2[C / 2];
+#endif
     f2 Ub[M][NS], Un[M][NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -1036,6 +1081,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // workgroup go to SIMD (wave index mod 4): the group's wave P3W lands
         // the G pass-3 waves evenly on the four SIMDs (the group's first wave
         // put them all on SIMD 0, or 0 and 2, one after another)
+        if constexpr (DM == 0 && decltype(rc)::value == 0)
+            pin_words();  // every wave, before the first round's output stores
         if ((jl >> 6) == P3W && pair_on) {
             const int l = jl & 63;
             const int mm = 64 - l;
@@ -1091,6 +1138,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             sa[h] = oka ? scl[pp[h] * K + ln] : 0.0f;
             sb[h] = okb ? scl[pp[h] * K + ln + 64] : 0.0f;
         }
+        pin_words();
         if (on2[0])
             frame16_pair_out<2>(kp, out, priorl, lagl, fr, P, pp, on2, ln, ln + 64, oka, okb, sa, sb, ln == 0, ep_lo,
                                 ep_w, ep_off);
@@ -1098,6 +1146,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (fr == diag_fr)
             F16_MARK();
     }
+    pin_words();
     if (tid == 0 && out.gate) {
         int tot = 0;
         for (int q = 0; q < P; q++)
