@@ -245,6 +245,10 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 // The stream states are requested at the kernel's start (ema_prefetch: the
 // thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
 // latency hides behind the staging and the xcorr.
+// waves per SIMD the streaming (EMA) kernel is compiled for: 6 caps it at 80 VGPRs
+#ifndef MF_EMA_WPE
+#define MF_EMA_WPE 6
+#endif
 constexpr int EMA_E = 3;  // state elements per thread: F P K <= EMA_E x threads (host-checked)
 
 struct EmaPre {
@@ -485,7 +489,7 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
 }
 
 template <bool PREPARED, int TWC, int CH, bool EMA>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA && CH <= 4 ? 6 : 1))) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA && CH <= 4 ? MF_EMA_WPE : 1))) k_direct_mfma(tdoa_kparams kp, tdoa_kout out,
                                                       const int16_t *__restrict__ frames, int64_t B,
                                                       const int32_t *__restrict__ count, int n0, int nq,
                                                       MfTabs tb, tdoa_stream_fuse ef)
