@@ -245,6 +245,10 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 // The stream states are requested at the kernel's start (ema_prefetch: the
 // thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
 // latency hides behind the staging and the xcorr.
+// the streaming kernel's grid tables requested after the xcorr (see k_direct_mfma)
+#ifndef MF_EMA_LATE_TABLES
+#define MF_EMA_LATE_TABLES 0
+#endif
 // waves per SIMD the streaming (EMA) kernel is compiled for: 6 caps it at 80 VGPRs
 #ifndef MF_EMA_WPE
 #define MF_EMA_WPE 6
@@ -515,14 +519,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     uint32_t gq[GR];
     int32_t gc[GR];
     const bool do_grid = out.cell || out.xy || out.max_L;
-    if constexpr (KEYGRID) {
+    auto grid_tables = [&] {
 #pragma unroll
         for (int r = 0; r < GR; r++) {
             const int u = (int)threadIdx.x + r * (int)blockDim.x;
             gq[r] = do_grid && u < kp.U ? kp.tuples[u] : 0u;
             gc[r] = do_grid && u < kp.U ? kp.tuple_cell[u] : 0;
         }
-    }
+    };
+    if constexpr (KEYGRID && !(EMA && MF_EMA_LATE_TABLES))
+        grid_tables();
     EmaPre epre{};
     if constexpr (EMA)
         epre = ema_prefetch(kp, ef.sp, f0, nf);
@@ -589,6 +595,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     }
     __syncthreads();
     DIAG_STAMP(3);
+    if constexpr (KEYGRID && EMA && MF_EMA_LATE_TABLES) {
+        // the streaming kernel requests its grid tables here, after the xcorr,
+        // and waits for them before the batch's first output store: held from
+        // the kernel's start they spilled at the 80-VGPR cap, and the reloads
+        // after the EMA stores waited for the stores' acknowledgements
+        grid_tables();
+#pragma unroll
+        for (int r = 0; r < GR; r++)
+            asm volatile("" : "+v"(gq[r]), "+v"(gc[r]));
+    }
     argmax_prior_mf<KEYGRID>(kp, sm.scores, sm.best, reinterpret_cast<const float *>(smem + tb.prior), out, f0, nf);
     DIAG_STAMP(4);
     // streaming: the EMA of the gated frames replaces their scores in LDS, and
