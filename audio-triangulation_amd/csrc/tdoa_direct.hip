@@ -245,9 +245,10 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 // The stream states are requested at the kernel's start (ema_prefetch: the
 // thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
 // latency hides behind the staging and the xcorr.
-// the streaming kernel's grid tables requested after the xcorr (see k_direct_mfma)
+// the streaming kernel's grid tables requested after the xcorr (see k_direct_mfma;
+// 81.35 -> 79.5 us per config-5 hop, same box)
 #ifndef MF_EMA_LATE_TABLES
-#define MF_EMA_LATE_TABLES 0
+#define MF_EMA_LATE_TABLES 1
 #endif
 // waves per SIMD the streaming (EMA) kernel is compiled for: 6 caps it at 80 VGPRs
 #ifndef MF_EMA_WPE
