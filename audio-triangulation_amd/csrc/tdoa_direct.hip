@@ -504,10 +504,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
     DIAG_STAMP(10);
     if (count) {  // batch size known on the device only (streaming pipeline)
-        const int64_t c = *count;
+        // at most B slots (one per stream): a corrupted counter is clamped
+        // before any reader (ema_hop's stats, the batch bound) sees it
+        int64_t c = *count;
+        c = c < 0 ? 0 : (c > B ? B : c);
         if constexpr (EMA)
             ema_hop(ef, (int)c);
-        B = c < B ? c : B;
+        B = c;
         if (f0 >= B)
             return;
     }

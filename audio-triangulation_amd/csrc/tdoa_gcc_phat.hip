@@ -690,23 +690,48 @@ bool tdoa_phat_r16_fits(int M, int N, int S);
 bool frame16_shape(const tdoa_kparams &kp);
 const char *frame16_kernel_name(const tdoa_kparams &kp);
 
-const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp)
+bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
+
+// The one dispatch decision of tdoa_launch_gcc_phat, shared with
+// tdoa_gcc_phat_kernel_name so the reported kernel is the launched one.
+enum class PhatRoute { W64, P1K_LEAN, R16, SPLIT, FUSED_1024, GENERIC };
+static PhatRoute phat_route(const tdoa_kparams &kp)
 {
     if (use_w64(kp))
-        return "k_p1k_w64";
+        return PhatRoute::W64;
     if (tdoa_phat1024_fits(kp))
-        return "k_p1k_lean";
+        return PhatRoute::P1K_LEAN;
+    // frame_len 2048 / 4096 with M > 3 or N > 2048: register-pass kernels
+    // (tdoa_phat_r16.hip); other long shapes the LDS Stockham pair
     if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
-        return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) ? (frame16_shape(kp) ? frame16_kernel_name(kp) : "k_spec16")
-                                                   : "k_phat_spectra";
+        return tdoa_phat_r16_fits(kp.M, kp.N, kp.S) ? PhatRoute::R16 : PhatRoute::SPLIT;
+    if (tdoa_gcc_phat_fused_grid(kp))
+        return PhatRoute::FUSED_1024;
+    return PhatRoute::GENERIC;
+}
+
+const char *tdoa_gcc_phat_kernel_name(const tdoa_kparams &kp)
+{
+    switch (phat_route(kp)) {
+    case PhatRoute::W64:
+        return "k_p1k_w64";
+    case PhatRoute::P1K_LEAN:
+        return "k_p1k_lean";
+    case PhatRoute::R16:
+        return frame16_shape(kp) ? frame16_kernel_name(kp) : "k_spec16";
+    case PhatRoute::SPLIT:
+        return "k_phat_spectra";
+    case PhatRoute::FUSED_1024:
+        return "k_gcc_phat_1024";
+    case PhatRoute::GENERIC:
+        break;
+    }
     return "k_gcc_phat";
 }
 int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                          float phat_eps, void *scratch, size_t scratch_bytes, void *stream);
 
 bool tdoa_phat_r16_peak3(const tdoa_kparams &kp);
-
-bool tdoa_gcc_phat_fused_grid(const tdoa_kparams &kp);
 
 // the launch solves the grid itself (no weighted-score scratch, no grid launch)
 bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp)
@@ -738,20 +763,19 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
         return tdoa_set_error(-1, "frames must be 16-byte aligned");
     if (!kp.tw || !kp.tw2)
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
-    if (use_w64(kp))
+    const PhatRoute route = phat_route(kp);
+    if (route == PhatRoute::W64)
         return tdoa_launch_p1k_w64(kp, out, frames, B, phat_eps, stream);
-    if (tdoa_phat1024_fits(kp))
+    if (route == PhatRoute::P1K_LEAN)
         return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
-    // frame_len 2048 / 4096 with M > 3 or N > 2048: register-pass kernels
-    // (tdoa_phat_r16.hip); other long shapes the LDS Stockham pair
-    if (tdoa_gcc_phat_needs_split(kp.M, kp.N) && tdoa_phat_r16_fits(kp.M, kp.N, kp.S))
+    if (route == PhatRoute::R16)
         return tdoa_launch_phat_r16(kp, out, frames, B, phat_eps, spec_scratch, spec_bytes, stream);
-    if (tdoa_gcc_phat_needs_split(kp.M, kp.N))
+    if (route == PhatRoute::SPLIT)
         return tdoa_launch_gcc_phat_split(kp, out, frames, B,
                                           eps2 * 1152921504606846976.0f /* 2^60: int16 units */,
                                           spec_scratch, spec_bytes, stream);
     hipStream_t st = (hipStream_t)stream;
-    if (tdoa_gcc_phat_fused_grid(kp)) {
+    if (route == PhatRoute::FUSED_1024) {
         // persistent 2-frame workgroups, as many as are resident at once
         // + grid tail: [3][128][8] scores, 8 frame indices, [3][8] reductions
         const size_t lds1024 = 7 * 1024 * 8 + 514 * 8 + 512 * 8 + 8 * 4 + 3 * 128 * GSLOTS * 4 +

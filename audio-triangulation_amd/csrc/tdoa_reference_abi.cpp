@@ -11,6 +11,9 @@
 // Host (capture ring / one-time geometry):
 //   rolling_buffer_init/push/get_*_power  rolling_buffer.c:3-41,73-85
 //   microphones_init                      microphones.c:9-33
+// tdoa_ref_set_device(-1) runs the GPU-backed five on libtdoa's own host-CPU
+// implementation instead (tdoa_host_path.cpp; BASELINE config 1 "on host CPU,
+// no GPU"): same results bit for bit, and no HIP call at all.
 
 #include "../../include/tdoa_reference_abi.h"
 #include "../../include/tdoa.h"
@@ -27,6 +30,15 @@
 #include <mutex>
 #include <time.h>
 
+namespace tdoa_host {
+void write_out(const int16_t *ring, int head, int16_t *dst, int64_t *power);
+void normalize(int16_t *buf);
+void window(int16_t *buf, const int16_t *w);
+void correlate(const int16_t *a, const int16_t *b, const float *prior, int64_t *corr, int *best);
+void average(int64_t *est, const int64_t *fresh, float decay, int *best);
+}  // namespace tdoa_host
+
+int tdoa_ctx_device(const tdoa_ctx *c);
 int tdoa_launch_ref_buffer(int op, int16_t *buf, const int16_t *ring, int head, int64_t *power,
                            const int16_t *window, int n, void *stream, int16_t *s1, int16_t *s2);
 
@@ -49,7 +61,33 @@ absolute_time_t default_clock()
 }
 
 absolute_time_t (*g_clock)(void) = default_clock;
-int g_device = 0;
+std::atomic<int> g_device{0};  // < 0: the host-CPU path (tdoa_host_path.cpp)
+
+bool host_mode() { return g_device.load(std::memory_order_relaxed) < 0; }
+
+// the host path's tables: the Q15 DPSS(1024, 2) window (window_function.h) and
+// the lag prior of correlations.c:27-30, built once with libm on the host
+struct HostTables {
+    int16_t window[TDOA_REF_BUFFER_SIZE];
+    float prior[TDOA_REF_CORR_SIZE];
+};
+const HostTables &host_tables()
+{
+    static const HostTables t = [] {
+        HostTables h;
+        int32_t w[TDOA_REF_BUFFER_SIZE];
+        if (tdoa_dpss_q15(TDOA_REF_BUFFER_SIZE, 2.0, w) != TDOA_OK) {
+            std::fprintf(stderr, "libtdoa reference shim: tdoa_dpss_q15 failed\n");
+            std::abort();
+        }
+        for (int i = 0; i < TDOA_REF_BUFFER_SIZE; i++)
+            h.window[i] = (int16_t)w[i];
+        for (int d = 0; d < TDOA_REF_CORR_SIZE; d++)
+            h.prior[d] = (float)std::exp((double)((float)(-(d * d)) / 36.f));
+        return h;
+    }();
+    return t;
+}
 
 // One lazily created 2-mic context (pair = (buf_a, buf_b)), its stream and
 // one block of pinned, device-mapped host memory the per-frame kernels read
@@ -102,9 +140,9 @@ RefState &ref()
     cfg.mic_xy = two_mics;
     cfg.grid_half_w = 0;
     cfg.grid_half_h = 0;
-    if (tdoa_create(&cfg, g_device, &g_ref.ctx) != TDOA_OK)
+    if (tdoa_create(&cfg, g_device.load(), &g_ref.ctx) != TDOA_OK)
         die("tdoa_create");
-    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipSetDevice(g_device.load()), "hipSetDevice");
     check(hipStreamCreateWithFlags(&g_ref.st, hipStreamNonBlocking), "hipStreamCreate");
     check(hipHostMalloc(reinterpret_cast<void **>(&g_ref.io), sizeof(HostIO),
                         hipHostMallocMapped | hipHostMallocCoherent),
@@ -159,7 +197,7 @@ void buffer_op(int op, struct buffer_t *dst, const struct rolling_buffer_t *ring
         if (memo_hit(op == 1 ? g_memo.norm : g_memo.win, dst->buffer))
             return;
     }
-    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipSetDevice(g_device.load()), "hipSetDevice");
     HostIO &io = *R.io;
     int16_t *buf = io.frames[0];
     if (ring)
@@ -195,9 +233,13 @@ extern "C" void tdoa_ref_set_clock(absolute_time_t (*now_us)(void))
 
 extern "C" int tdoa_ref_set_device(int device)
 {
-    if (g_ref.ready.load(std::memory_order_acquire))
+    // -1 (any negative): the host-CPU path, selectable at any time; a GPU
+    // device only before the first GPU-backed call (its context is bound to it),
+    // or the device already in use
+    if (device >= 0 && g_ref.ready.load(std::memory_order_acquire) && g_ref.ctx &&
+        device != tdoa_ctx_device(g_ref.ctx))
         return TDOA_ERR_INVALID;
-    g_device = device;
+    g_device = device < 0 ? -1 : device;
     return TDOA_OK;
 }
 
@@ -260,18 +302,41 @@ extern "C" power_t rolling_buffer_get_outgoing_power(const struct rolling_buffer
 // ------------------------------------------------------------- GPU-backed
 extern "C" void rolling_buffer_write_out(const struct rolling_buffer_t *b, struct buffer_t *dst)
 {
+    if (host_mode()) {
+        tdoa_host::write_out(b->buffer, b->head, dst->buffer, &dst->power);
+        return;
+    }
     buffer_op(0, dst, b);
 }
 
-extern "C" void buffer_normalize_range(struct buffer_t *buf) { buffer_op(1, buf, nullptr); }
+extern "C" void buffer_normalize_range(struct buffer_t *buf)
+{
+    if (host_mode()) {
+        tdoa_host::normalize(buf->buffer);
+        return;
+    }
+    buffer_op(1, buf, nullptr);
+}
 
-extern "C" void buffer_window(struct buffer_t *buf) { buffer_op(2, buf, nullptr); }
+extern "C" void buffer_window(struct buffer_t *buf)
+{
+    if (host_mode()) {
+        tdoa_host::window(buf->buffer, host_tables().window);
+        return;
+    }
+    buffer_op(2, buf, nullptr);
+}
 
 extern "C" void correlations_init(struct correlations_t *corr, const struct buffer_t *a,
                                   const struct buffer_t *b)
 {
+    if (host_mode()) {
+        tdoa_host::correlate(a->buffer, b->buffer, host_tables().prior, corr->correlations, &corr->best_shift);
+        corr->last_update = g_clock();
+        return;
+    }
     RefState &R = ref();
-    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipSetDevice(g_device.load()), "hipSetDevice");
     HostIO &io = *R.io;
     std::memcpy(io.frames[0], a->buffer, sizeof a->buffer);
     std::memcpy(io.frames[1], b->buffer, sizeof b->buffer);
@@ -289,8 +354,15 @@ extern "C" void correlations_init(struct correlations_t *corr, const struct buff
 
 extern "C" void correlations_average(struct correlations_t *est, struct correlations_t *fresh)
 {
+    if (host_mode()) {
+        const absolute_time_t now = g_clock();
+        tdoa_host::average(est->correlations, fresh->correlations, tdoa_decay_us(now, est->last_update),
+                           &est->best_shift);
+        est->last_update = now;
+        return;
+    }
     RefState &R = ref();
-    check(hipSetDevice(g_device), "hipSetDevice");
+    check(hipSetDevice(g_device.load()), "hipSetDevice");
     HostIO &io = *R.io;
     const absolute_time_t now = g_clock();
     int64_t *h_est = io.i64, *h_new = io.i64 + 128;

@@ -244,7 +244,13 @@ extern "C" int tdoa_stream_step(tdoa_stream *st, const tdoa_stream_outputs *out,
         st->g_out[par] = want;
         st->g_stream[par] = s;
     }
-    S_TRY(hipGraphLaunch(st->exec[par], s));
+    const hipError_t el = hipGraphLaunch(st->exec[par], s);
+    if (el != hipSuccess) {
+        // as in the eager path: a partly run hop may have counted into its
+        // slot; both slots are zeroed so the next hop starts from slot 0
+        (void)hipMemsetAsync(st->sp.count, 0, 2 * sizeof(int32_t), s);
+        return sfail(TDOA_ERR_HIP, "hipGraphLaunch: %s", hipGetErrorString(el));
+    }
     st->hop++;
     return TDOA_OK;
 }

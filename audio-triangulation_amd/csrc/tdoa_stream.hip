@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
 __device__ __forceinline__ float decay_us(uint64_t now, uint64_t last) { return tdoa_decay_dev(now, last); }
 
 __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, tdoa_kparams kp,
-                                                       tdoa_stream_kout out)
+                                                       tdoa_stream_kout out, int nstreams)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int64_t *W = (int64_t *)smem;     // [P][K] EMA scores
@@ -476,7 +476,9 @@ __global__ void __launch_bounds__(TPB) k_stream_update(tdoa_stream_params sp, td
     __shared__ uint64_t redk[TPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = TPB / 64;
     const int K = kp.K, P = kp.P;
-    const int cnt = *sp.count;
+    // at most one slot per stream: a corrupted counter cannot index past [S]
+    const int cnt_raw = *sp.count;
+    const int cnt = cnt_raw < 0 ? 0 : (cnt_raw > nstreams ? nstreams : cnt_raw);
     if (blockIdx.x == 0) {
         // gated frames of this hop: block 0 sums the batch's gate bytes (a
         // per-slot atomic on one counter serialises in L2)
@@ -727,7 +729,7 @@ int tdoa_launch_stream_update(const tdoa_stream_params &sp, const tdoa_kparams &
     const size_t lds = (size_t)kp.P * kp.K * 8;
     const int64_t grid = S < 2048 ? S : 2048;  // persistent: up to 8 workgroups per CU
     hipLaunchKernelGGL(k_stream_update, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(TPB), lds, (hipStream_t)stream, sp,
-                       kp, out);
+                       kp, out, (int)S);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail_hip(e, "k_stream_update launch");
 }

@@ -92,11 +92,17 @@ def barrier() -> None:
         dist.barrier()
 
 
+def _coll_device(device):
+    """Where a reduction's tensor lives: the rank's GPU under RCCL, the host
+    under gloo (a CPU process group, also when the ranks hold GPUs)."""
+    return None if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(x: float, device=None) -> float:
     """Max of a scalar over all ranks (the bench's whole-job time)."""
     if not _active():
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -106,7 +112,7 @@ def sum_over_ranks(xs, device=None) -> list[float]:
     xs = [float(x) for x in xs]
     if not _active():
         return xs
-    t = torch.tensor(xs, dtype=torch.float64, device=device)
+    t = torch.tensor(xs, dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(v) for v in t.tolist()]
 

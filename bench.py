@@ -120,6 +120,11 @@ def parse():
                     help="no GPU: rehearse the N-process launch, rank logic and JSON line over gloo "
                          "with a stand-in CPU step (tests/test_distributed.py); not a measurement")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend at N > 1 (nccl = RCCL; gloo: the N-rank code on one "
+                         "GPU box, e.g. with --rank-device 0; never a measurement of N GPUs)")
+    ap.add_argument("--rank-device", type=int, default=-1,
+                    help="GPU of every rank (default: LOCAL_RANK, one GPU per rank)")
     ap.add_argument("--also", action="store_true", help="also time the other engine")
     ap.add_argument("--no-grid", action="store_true", help="diagnostic: skip the grid solve")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
@@ -332,26 +337,27 @@ def time_stream(args, dev, ri, cache):
             "latency_ms": {"p50": pct(lat_host, 50), "p99": pct(lat_host, 99),
                            "gpu_p50": pct(lat_gpu, 50), "gpu_p99": pct(lat_gpu, 99),
                            "hops": len(lat_host),
-                           "kind": "per hop, one hop in flight: submit -> results on the host "
-                                   "(p50/p99), and the hop's GPU time from events (gpu_*); "
+                           "kind": "per hop, one hop in flight: submit -> the hop's device outputs "
+                                   "complete (graph replay, kernels, stream synchronise; no copy to the "
+                                   "host) (p50/p99), and the hop's GPU time from events (gpu_*); "
                                    "measured after the timed region"}}
 
 
-def time_config1(args, dev, ri):
+def time_config1(args, dev, ri, path):
     """Config 1: one 2-mic frame per step through the reference-named entry
     points of tdoa_reference_abi.h -- rolling_buffer_write_out, buffer_normalize_range,
     buffer_window for both buffers, then correlations_init (sample_compute.h:105-122
-    for one pair): seven GPU-backed per-frame calls, each a synchronous round trip
-    of the reference struct.  Every frame's correlations and best shift are checked
-    against the oracle after the timed region."""
+    for one pair): seven per-frame calls on the reference structs.  path "host":
+    libtdoa's own host-CPU implementation (tdoa_ref_set_device(-1),
+    csrc/tdoa_host_path.cpp; BASELINE config 1 is "on host CPU, no GPU"); path
+    "gpu": each call a synchronous GPU round trip.  Every frame's correlations
+    and best shift are checked against the oracle after the timed region."""
     import ctypes as C
     import tdoa
     from tdoa import _lib, synth
     from tdoa.localizer import Localizer
     cfg = CONFIGS[1]
     L = tdoa.load()
-    if L.tdoa_ref_set_device(int(dev.index)) != 0:
-        raise RuntimeError("tdoa_ref_set_device failed")
     loc = Localizer(engine="direct", num_mics=2, frame_len=1024, mic_xy=config_mics(cfg),
                     device=dev.index)
     S = loc.dims.S
@@ -372,21 +378,28 @@ def time_config1(args, dev, ri):
         rings.append(pair)
     outs = [_lib.Correlations() for _ in range(n)]
     ba, bb = _lib.Buffer(), _lib.Buffer()
+    wo, nr, wi, ci = (L.rolling_buffer_write_out, L.buffer_normalize_range, L.buffer_window,
+                      L.correlations_init)
 
     def step(i):
         ra, rb = rings[i]
-        L.rolling_buffer_write_out(C.byref(ra), C.byref(ba))
-        L.rolling_buffer_write_out(C.byref(rb), C.byref(bb))
-        L.buffer_normalize_range(C.byref(ba))
-        L.buffer_normalize_range(C.byref(bb))
-        L.buffer_window(C.byref(ba))
-        L.buffer_window(C.byref(bb))
-        L.correlations_init(C.byref(outs[i]), C.byref(ba), C.byref(bb))
+        wo(C.byref(ra), C.byref(ba))
+        wo(C.byref(rb), C.byref(bb))
+        nr(C.byref(ba))
+        nr(C.byref(bb))
+        wi(C.byref(ba))
+        wi(C.byref(bb))
+        ci(C.byref(outs[i]), C.byref(ba), C.byref(bb))
 
-    for i in range(args.warmup):
-        step(i)
-    t = shard.timed(lambda k: step(args.warmup + k), args.steps, 0,
-                    sync=lambda: torch.cuda.synchronize(dev), device=dev)
+    if L.tdoa_ref_set_device(-1 if path == "host" else int(dev.index)) != 0:
+        raise RuntimeError("tdoa_ref_set_device failed")
+    try:
+        for i in range(args.warmup):
+            step(i)
+        sync = (lambda: None) if path == "host" else (lambda: torch.cuda.synchronize(dev))
+        t = shard.timed(lambda k: step(args.warmup + k), args.steps, 0, sync=sync, device=dev)
+    finally:
+        L.tdoa_ref_set_device(int(dev.index))
     total = shard.sum_over_ranks([args.steps], device=dev)[0]
     # parity: the oracle's DC removal / normalise / window / xcorr / prior per frame
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -425,12 +438,13 @@ def cpu_baseline_config1(args, res):
 
 
 def main_config1(args, dev, ri):
-    res = time_config1(args, dev, ri)
+    res = time_config1(args, dev, ri, "host")
+    gpu = time_config1(args, dev, ri, "gpu")
     world = shard.ranks_seen()
     if ri.rank == 0:
         cfg = CONFIGS[1]
         line = {
-            "metric": "localizations/sec (2-mic DIRECT xcorr, reference per-frame entry points)",
+            "metric": "localizations/sec (2-mic DIRECT xcorr, reference per-frame entry points, host CPU)",
             "value": res["value"], "unit": "localizations/s", "n_gpus": world, "ranks_seen": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -438,13 +452,18 @@ def main_config1(args, dev, ri):
             "data": "synthetic (ADC-like u8 frames, injected integer delays) in host rolling-buffer "
                     "structs, as the reference's capture side leaves them",
             "config": {"workload": f"{cfg['desc']}, one frame per step", "mics": 2, "frame_len": 1024,
-                       "calls_per_frame": 7, "parallelism": f"dp{world} (per-frame, no collective)"},
+                       "calls_per_frame": 7, "path": "libtdoa host-CPU path (tdoa_ref_set_device(-1), "
+                                                     "csrc/tdoa_host_path.cpp, AVX2), one thread",
+                       "parallelism": f"dp{world} (per-frame, no collective)"},
             "parity": res["parity"],
             "roofline": None,
-            "note": "latency-bound plumbing: seven synchronous GPU-backed calls per frame, three GPU "
-                    "round trips (each write_out's launch also computes the buffer's normalize and "
-                    "window, returned by those calls when their buffer holds exactly write_out's "
-                    "output); the batched API is configs 2-5",
+            "gpu_backed": {"value": gpu["value"], "ms_per_step": gpu["ms_per_step"], "parity": gpu["parity"],
+                           "note": "the same seven calls with the GPU-backed symbols (default device): "
+                                   "latency-bound, three GPU round trips per frame (each write_out's "
+                                   "launch also computes the buffer's normalize and window); the batched "
+                                   "API is configs 2-5"},
+            "note": "BASELINE config 1 is defined on the host CPU: the line's value is libtdoa's own host "
+                    "path (no HIP call); cpu_baseline is the oracle port of the same sequence",
             "cpu_baseline": cpu_baseline_config1(args, res) if not args.no_cpu else None,
         }
         print(json.dumps(line), flush=True)
@@ -649,9 +668,9 @@ def main():
         sys.exit(3)
     if args.cpu_rehearsal:
         return rehearse(args)
-    ri = shard.init_distributed("nccl")
+    ri = shard.init_distributed(args.dist_backend)
     check_world(args, "process group")
-    dev = torch.device("cuda", ri.local_rank)
+    dev = torch.device("cuda", ri.local_rank if args.rank_device < 0 else args.rank_device)
     torch.cuda.set_device(dev)
     cache = {}
     if args.config == 5:

@@ -23,6 +23,10 @@
  *     or tdoa_ref_set_device); they never fall back to a CPU path -- a HIP
  *     failure prints the reason and aborts, since the reference functions
  *     return void.  Throughput work goes through tdoa.h's batched API.
+ *   - tdoa_ref_set_device(-1) explicitly selects libtdoa's own host-CPU
+ *     implementation of those five (csrc/tdoa_host_path.cpp, bit-exact, no
+ *     HIP call; BASELINE config 1 "on host CPU"); tdoa_ref_set_device(0)
+ *     switches back.
  *   - rolling_buffer_init / push / get_*_power are the per-sample capture
  *     ring (the ADC/DMA side, sample_compute.h:62-99) and run on the host.
  *   - microphones_init is one-time geometry and runs on the host.
@@ -98,7 +102,9 @@ void correlations_average(struct correlations_t *estimate, struct correlations_t
 
 /* libtdoa extensions for the per-frame shim */
 void tdoa_ref_set_clock(absolute_time_t (*now_us)(void));
-int tdoa_ref_set_device(int device); /* before the first GPU-backed call */
+/* device >= 0: before the first GPU-backed call (or the device in use);
+ * device < 0: the host-CPU path, at any time */
+int tdoa_ref_set_device(int device);
 
 #ifdef __cplusplus
 }
