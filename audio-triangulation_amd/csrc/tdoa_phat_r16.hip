@@ -104,6 +104,45 @@ __host__ __device__ constexpr int po(int o) { return o + (o >> 4); }
 __device__ __forceinline__ f2 lds2(const f2 *buf, int i) { return buf[pidx(i)]; }
 __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 
+// k_frame16's transform buffers (F16_XS, default): element i at xs(i) =
+// i ^ ((i >> 4) & 15), a permutation inside each aligned 16-element block, no
+// padding.  The padded layout (pidx: i + i/16) keeps the 16-lane stride-16
+// writes conflict-free, but every 32-lane ds_read_b64 of 32 consecutive
+// elements spans 33 slots there, so its first and last lanes share a bank
+// (2-way, the read's 2 LDS cycles become 3+).  The swizzle is conflict-free
+// for both: a consecutive read stays a permutation of its two aligned 16-blocks,
+// and the stride-16 writes 16 j + r land on slots r ^ (j & 15).  Every access
+// below is a per-thread base and a compile-time part (an offset, or one XOR)
+// -- see ColIdx and the pass writes.  The padding's C / 16 elements per buffer
+// are freed (8 KiB at config 4).
+#ifndef F16_XS
+#define F16_XS 1
+#endif
+__host__ __device__ constexpr int xs(int i) { return i ^ ((i >> 4) & 15); }
+template <bool XS>
+__host__ __device__ constexpr int lidx(int i) { return XS ? xs(i) : pidx(i); }
+// buffer length in elements (one group's transform)
+template <int C, bool XS>
+constexpr int f16_buf() { return XS ? C : C + C / 16; }
+// element j + T r (T = C / 16, j < T, r a compile-time constant after
+// unrolling) of a group buffer: xs(j + T r) = T r + (xs(j) ^ ((T r >> 4) & 15)),
+// which is xs(j) + T r at T = 256 and (xs(j) ^ 8 (r & 1)) + T r at T = 128
+template <int C, bool XS>
+struct ColIdx {
+    int b0, b1;
+    __device__ __forceinline__ explicit ColIdx(int j)
+    {
+        static_assert(C == 2048 || C == 4096, "k_frame16 shapes");
+        b0 = XS ? xs(j) : pidx(j);
+        b1 = XS && C == 2048 ? (b0 ^ 8) : b0;
+    }
+    __device__ __forceinline__ int at(int r) const
+    {
+        constexpr int T = C / 16;
+        return XS ? ((r & 1) ? b1 : b0) + T * r : b0 + po(T * r);
+    }
+};
+
 template <int R>
 __device__ constexpr int brev(int k)
 {
@@ -537,12 +576,13 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 // ends in buf at pidx(j + T q), after a closing barrier
 // WM: where the thread's window words come from -- 0 global (L2), 1 LDS (win
 // is the LDS copy), 2 registers (wr, loaded once per launch)
-template <int C, int WM, typename Mark>
+template <int C, int WM, typename Mark, bool XS = false>
 __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, const uint32_t (&wr)[8],
                                                 f2 *buf, int *red, const f2 *tt, int tid, int g, int j, int pj,
                                                 int log2N, Mark mark)
 {
     constexpr int T = C / 16, R1 = C / 256;
+    const ColIdx<C, XS> cj(j);  // XS: pj is unused (the column reads / writes go through cj)
     uint32_t wn[8];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
@@ -582,9 +622,11 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         for (int s = 8; s < 16; s++)
             v[s] = f2{0.0f, 0.0f};
         dftp<16, false, true>(v);
+        // element 16 j + r: pidx = 17 j + r; xs = (16 j | (j & 15)) ^ r
+        const int b1 = 16 * j | (j & 15);
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            buf[17 * j + r] = v[brev<16>(r)];  // pidx(16 j + r)
+            buf[XS ? (b1 ^ r) : 17 * j + r] = v[brev<16>(r)];
     } else {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -596,10 +638,12 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             for (int r = 4; r < 8; r++)
                 u[r] = f2{0.0f, 0.0f};
             dftp<8, false, true>(u);
-            // pidx(8 (j + 128 h) + r) = 8 j + (j >> 1) + 1088 h + r (r < 8)
+            // element 8 (j + 128 h) + r (r < 8): pidx = 8 j + (j >> 1) + 1088 h + r;
+            // xs = 1024 h + ((16 (j >> 1) | (8 (j & 1) ^ ((j >> 1) & 15))) ^ r)
+            const int b2 = 16 * (j >> 1) | ((8 * (j & 1)) ^ ((j >> 1) & 15));
 #pragma unroll
             for (int r = 0; r < 8; r++)
-                buf[8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
+                buf[XS ? 1024 * h + (b2 ^ r) : 8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
         }
     }
     __syncthreads();
@@ -608,25 +652,31 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         const int k = j % R1;
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            v[r] = F16_LD(buf + pj + po(T * r));
+            v[r] = F16_LD(buf + (XS ? cj.at(r) : pj + po(T * r)));
 #pragma unroll
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
         dftp<16, false, false>(v);
         __syncthreads();
     mark();
-        // o mod 16 = k < R1: pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16
+        // element (j / R1) 16 R1 + k + R1 r.  pad: o mod 16 = k < R1, so
+        // pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16.  xs: the lane part
+        // (256 (j / 16) | k at R1 = 16; 128 (j / 8) | 8 ((j / 8) & 1) | k at R1 = 8)
+        // XOR a compile-time part (17 r; 16 (r / 2) | 8 (r & 1) | r / 2)
         const int o = pidx((j / R1) * 16 * R1 + k);
+        const int lv = R1 == 16 ? (256 * (j / 16) | k) : (128 * (j / 8) | 8 * ((j / 8) & 1) | k);
 #pragma unroll
-        for (int r = 0; r < 16; r++)
-            buf[o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
+        for (int r = 0; r < 16; r++) {
+            const int cr = R1 == 16 ? 17 * r : (16 * (r / 2) | 8 * (r & 1) | (r / 2));
+            buf[XS ? (lv ^ cr) : o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
+        }
     }
     __syncthreads();
     mark();
     {
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            v[r] = F16_LD(buf + pj + po(T * r));
+            v[r] = F16_LD(buf + (XS ? cj.at(r) : pj + po(T * r)));
 #if F16_TWPOW
         {
             // W_C^{r j}, r = 1..15, as powers of W_C^j (the tables give W_C^j
@@ -651,17 +701,17 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
     mark();
 #pragma unroll
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
-            buf[pj + po(T * q)] = v[brev<16>(q)];
+            buf[XS ? cj.at(q) : pj + po(T * q)] = v[brev<16>(q)];
     }
     __syncthreads();
     mark();
 }
 
 // LDS bytes of k_frame16
-template <int C>
+template <int C, bool XS = (F16_XS != 0)>
 constexpr size_t frame16_lds_base()
 {
-    constexpr int G = 16384 / C, BUF = C + C / 16;
+    constexpr int G = 16384 / C, BUF = f16_buf<C, XS>();
     return (size_t)G * BUF * sizeof(f2) + G * sizeof(f2) + 16 * 4 + TDOA_MAX_PAIRS * 4 +
            3 * 16 * 16 * sizeof(f2) + 128 * sizeof(float) + (size_t)(C / 256) * 64 * sizeof(f2) +
            (f16_win_lds<C>() ? (size_t)C * 2 : 0);
@@ -785,12 +835,12 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
 // wave per pair in parallel.  (Running the earlier rounds' epilogue on the
 // last round's idle groups instead measured slower at config 3: 3.865 vs
 // 3.826 ms per step.)
-template <int C, int M, int DM>
+template <int C, int M, int DM, bool XS = (F16_XS != 0)>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, int64_t B,
                                                      float e2)
 {
-    constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = C + C / 16;
+    constexpr int T = C / 16, R1 = C / 256, G = 16384 / C, NS = C / 2048, BUF = f16_buf<C, XS>();
     static_assert(M >= 2 && M <= G, "one forward round: every mic has its own group");
     constexpr int P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G;
     constexpr int WPG = T / 64;  // waves per group (4 or 2)
@@ -931,11 +981,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 
     // ---- 1. forward transform of mic g (k_spec16's passes in slot g)
-    frame16_forward<C, f16_win_mode<C>()>(w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N,
-                                         [&] {
+    auto fwd_mark = [&] {
         if (fr == diag_fr)
             F16_MARK();  // the forward's barriers (diagnostic build)
-    });
+    };
+    frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS>(w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt,
+                                                                    tid, g, j, pj, kp.log2N, fwd_mark);
     if (fr == diag_fr)
         F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
@@ -955,7 +1006,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const int b = tid + 1024 * s;
-        const int pb = pidx(b), pp = pidx((C - b) & (C - 1));
+        const int pb = lidx<XS>(b), pp = lidx<XS>((C - b) & (C - 1));
         const f2 wb = twb[s];
 #pragma unroll
         for (int m = 0; m < M; m++) {
@@ -968,7 +1019,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
     }
     if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
-        const f2 zh = lds2(bufs + tid * BUF, C / 2);
+        const f2 zh = bufs[tid * BUF + lidx<XS>(C / 2)];
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
     }
     __syncthreads();  // slots consumed: they become the pairs' buffers
@@ -985,14 +1036,15 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     static_for<0, ROUNDS>([&](auto rc) {
         constexpr int p0 = decltype(rc)::value * G;
         const int tl = opaque_idx(tid), jl = tl - g * T, pjl = pidx(jl);
+        const ColIdx<C, XS> cjl(jl);
         // this thread's Y slots b = tl + 1024 s and C - b (b = 0: C / 2, whose
         // value thread 0 writes after, in program order)
         int yb0[NS], yb1[NS];
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int b = tl + 1024 * s;
-            yb0[s] = pidx(b);
-            yb1[s] = b == 0 ? pidx(C / 2) : pidx(C - b);
+            yb0[s] = lidx<XS>(b);
+            yb1[s] = b == 0 ? lidx<XS>(C / 2) : lidx<XS>(C - b);
         }
         // packed inverse input Y of pair p0 + gg into buffer gg (all threads)
         static_for<0, G>([&](auto gc) {
@@ -1011,8 +1063,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 }
                 if (tl == 0) {  // Y[C/2] from R[C/2] alone
                     const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
-                    sts2(yb, C / 2,
-                         c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), twh)));
+                    yb[lidx<XS>(C / 2)] = c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), twh));
                 }
             }
         });
@@ -1029,16 +1080,17 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on) {
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                v[r] = F16_LD(buf + pjl + po(T * r));
+                v[r] = F16_LD(buf + (XS ? cjl.at(r) : pjl + po(T * r)));
             dftp<16, true, false>(v);
         }
         __syncthreads();
         if (fr == diag_fr)
             F16_MARK();
         if (on) {
+            const int b1 = 16 * jl | (jl & 15);  // xs(16 jl + r) = b1 ^ r
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                buf[17 * jl + r] = v[brev<16>(r)];
+                buf[XS ? (b1 ^ r) : 17 * jl + r] = v[brev<16>(r)];
         }
         __syncthreads();
         if (fr == diag_fr)
@@ -1050,9 +1102,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
-            f2 l0 = F16_LD(buf + pjl + po(T * r)), l1 = F16_LD(buf + pjl + po(T * (r + 4)));
-            const f2 h0 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 8))), F16_TW256(r + 8));
-            const f2 h1 = c_mulconj(F16_LD(buf + pjl + po(T * (r + 12))), F16_TW256(r + 12));
+            f2 l0 = F16_LD(buf + (XS ? cjl.at(r) : pjl + po(T * r)));
+            f2 l1 = F16_LD(buf + (XS ? cjl.at(r + 4) : pjl + po(T * (r + 4))));
+            const f2 h0 = c_mulconj(F16_LD(buf + (XS ? cjl.at(r + 8) : pjl + po(T * (r + 8)))), F16_TW256(r + 8));
+            const f2 h1 = c_mulconj(F16_LD(buf + (XS ? cjl.at(r + 12) : pjl + po(T * (r + 12)))), F16_TW256(r + 12));
             if (r)
                 l0 = c_mulconj(l0, F16_TW256(r));  // tw256
             l1 = c_mulconj(l1, F16_TW256(r + 4));
@@ -1068,11 +1121,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (fr == diag_fr)
             F16_MARK();
         if (on) {
-            const int o = pidx((jl >> 4) * 64 + k);  // + po(16 c) = 17 c
+            // element 64 a + 16 c + k (a = jl >> 4, c < 4): pidx = pidx(64 a + k) + 17 c;
+            // xs = (64 a | (k ^ (4 a & 15))) ^ 17 c
+            const int o = XS ? (64 * (jl >> 4) | (k ^ (4 * (jl >> 4) & 15))) : pidx((jl >> 4) * 64 + k);
             buf[o] = x0;
-            buf[o + 17] = x1;
-            buf[o + 34] = x14;
-            buf[o + 51] = x15;
+            buf[XS ? o ^ 17 : o + 17] = x1;
+            buf[XS ? o ^ 34 : o + 34] = x14;
+            buf[XS ? o ^ 51 : o + 51] = x15;
         }
         __syncthreads();
         if (fr == diag_fr)
@@ -1088,14 +1143,15 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int mm = 64 - l;
             // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
             // the output index C - m; tw3 holds each lane's factors (conjugated for l < 32)
-            const int pl = pidx(l);
+            // element l + 64 r: pidx = pidx(l) + 68 r; xs = (xs(l) ^ 4 (r & 3)) + 64 r
+            const int pl = lidx<XS>(l);
             // the R1 terms summed as a tree (a running sum was a dependent
             // chain of R1 - 1 complex products and adds on the round's critical path)
             f2 t[R1];
             t[0] = F16_LD(buf + pl);
 #pragma unroll
             for (int r = 1; r < R1; r++)
-                t[r] = c_mul(F16_LD(buf + pl + 68 * r), F16_LD(tw3 + 64 * r + l));
+                t[r] = c_mul(F16_LD(buf + (XS ? (pl ^ (4 * (r & 3))) + 64 * r : pl + 68 * r)), F16_LD(tw3 + 64 * r + l));
 #pragma unroll
             for (int h = R1 / 2; h >= 1; h >>= 1)
 #pragma unroll
