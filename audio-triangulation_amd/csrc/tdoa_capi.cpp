@@ -222,6 +222,8 @@ struct tdoa_ctx {
     void *d_tscratch = nullptr;  // [B][P][3] float peak scores (least squares)
     size_t tscratch_bytes = 0;
     std::vector<uint8_t> bb_img;  // k_grid_bb tables: tiles | ranges | tuples | uidx | queries
+    std::vector<uint16_t> bb_rng; // [NT][P] lo | hi << 8 (host copy)
+    void *d_fgq = nullptr;        // kp.fg_q
     int bb_wide = 0;              // a range wider than the queries encode: no k_grid_bb
     void *d_bb = nullptr;
     void *d_wc = nullptr;         // compact weighted-score chunk table (kp.wc_chunks)
@@ -384,6 +386,7 @@ void build_bb_tiles(tdoa_ctx *c)
         }
     const int NT = (int)tile.size() / 2;
     c->bb_NT = NT;
+    c->bb_rng = rng;
     c->bb_wide = 0;
     for (const uint16_t q : qry)
         c->bb_wide |= (q & 0x1FFF) == 0x1FFF;
@@ -410,6 +413,8 @@ void free_device(tdoa_ctx *c)
     (void)hipFree(c->d_bb);
     (void)hipFree(c->d_wc);
     c->d_wc = nullptr;
+    (void)hipFree(c->d_fgq);
+    c->d_fgq = nullptr;
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_p1k_img);
     c->d_p1k_img = nullptr;
@@ -757,6 +762,46 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             kp.wc_CK = off;
             kp.wc_nch = (int32_t)c->wc_chunks.size();
             kp.wc_chunks = (const uint32_t *)c->d_wc;
+            // the fused k_frame16 grid's queries (tdoa_internal.h, kp.fg_q)
+            std::vector<uint16_t> fq((size_t)kp.bb_NT * 32, 0);
+            bool fok = off <= 2048 && kp.bb_NT <= 256 && c->P <= 32;
+            for (int t = 0; fok && t < kp.bb_NT; t++)
+                for (int p = 0; p < c->P; p++) {
+                    const int lo = c->bb_rng[(size_t)t * c->P + p] & 0xFF, hi = c->bb_rng[(size_t)t * c->P + p] >> 8;
+                    const int n = hi - lo + 1;
+                    if (n < 1 || n > 15 || lo < kp.wc_lo[p] || hi >= kp.wc_lo[p] + kp.wc_w[p]) {
+                        fok = false;
+                        break;
+                    }
+                    const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
+                    const int e = kp.wc_off[p] + lo - kp.wc_lo[p];
+                    fq[(size_t)t * 32 + p] = (uint16_t)(e | (lv << 11) | ((n - (1 << lv)) << 13));
+                }
+            // ... and the regrouped tuples (bb order) as compact element indices,
+            // so a tuple's gathers need no per-pair offsets: [U][32] u16
+            const size_t qbytes = fq.size() * 2;
+            if (fok) {
+                const uint32_t *bt = (const uint32_t *)(c->bb_img.data() + (((size_t)kp.bb_NT * 8 + 15) & ~(size_t)15) +
+                                                        ((((size_t)kp.bb_NT * c->P * 2) + 15) & ~(size_t)15));
+                for (int u = 0; u < c->U; u++)
+                    for (int p = 0; p < c->P; p++) {
+                        const int lag = (bt[(size_t)u * c->TW + p / 4] >> (8 * (p & 3))) & 0xFF;
+                        fq.push_back((uint16_t)(kp.wc_off[p] + lag - kp.wc_lo[p]));
+                    }
+                fq.resize((size_t)kp.bb_NT * 32 + (size_t)c->U * 32, 0);
+                // (rows of 32: the pushes above are P per tuple; re-lay them out)
+                std::vector<uint16_t> tup((size_t)c->U * 32, 0);
+                for (int u = 0; u < c->U; u++)
+                    for (int p = 0; p < c->P; p++)
+                        tup[(size_t)u * 32 + p] = fq[(size_t)kp.bb_NT * 32 + (size_t)u * c->P + p];
+                std::copy(tup.begin(), tup.end(), fq.begin() + (size_t)kp.bb_NT * 32);
+            }
+            if (fok && hipMalloc(&c->d_fgq, fq.size() * 2) == hipSuccess &&
+                hipMemcpy(c->d_fgq, fq.data(), fq.size() * 2, hipMemcpyHostToDevice) == hipSuccess) {
+                kp.fg_q = (const uint16_t *)c->d_fgq;
+                kp.fg_tup = (const uint16_t *)((const char *)c->d_fgq + qbytes);
+                kp.fg_ok = 1;
+            }
         }
     }
     *out = c;
@@ -1030,6 +1075,16 @@ extern "C" const char *tdoa_batch_kernel(const tdoa_ctx *ctx)
     if (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT)
         return tdoa_gcc_phat_kernel_name(ctx->kp);
     return tdoa_direct_fused_grid(ctx->kp) ? "k_direct_mfma" : "k_direct";
+}
+
+extern "C" int tdoa_batch_grid_fused(const tdoa_ctx *ctx)
+{
+    if (!ctx)
+        return 0;
+    return (ctx->cfg.engine == TDOA_ENGINE_GCC_PHAT ? tdoa_gcc_phat_grid_in_kernel(ctx->kp)
+                                                    : tdoa_direct_fused_grid(ctx->kp))
+               ? 1
+               : 0;
 }
 
 extern "C" int tdoa_abi_version(void) { return TDOA_ABI_VERSION; }

@@ -94,7 +94,13 @@ __global__ void __launch_bounds__(1024) k_direct(tdoa_kparams kp, tdoa_kout out,
 // 4 (l >> 4) + e of column l & 15.
 constexpr int MF_GR = 4;      // keyed grid: tuple words held per thread (the 16-wave form)
 constexpr int MF_GR_EMA = 5;  // ... and in the 8-wave streaming workgroup (U <= 5 x 512)
-constexpr int MF_PADW = 96;  // zero words each side of a staged row (b reads reach N + 175 samples)
+// zero words each side of a staged row: 2 PADW bytes per plane and side.  For
+// S <= 63 the a reads span [-16, N + 68) and the b reads [-64, N + 112) samples
+// (a: q0 = 64 beta + 16 g - r >= -15, five dwords from q0 & ~3; b: qb = 64 beta
+// + 16 (g + rr - n0), rr - n0 <= ceil((S + 1) / 16) - 1 <= 3, one 16-B read), so
+// 56 words (112 bytes) suffice; 2 PADW stays a multiple of 16 (aligned b reads).
+// (96 before round 5: the config-5 workgroup's 44.6 KB of LDS allowed 3 per CU)
+constexpr int MF_PADW = 56;
 
 typedef int v4i_mf __attribute__((ext_vector_type(4)));
 
@@ -252,7 +258,7 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 #endif
 // waves per SIMD the streaming (EMA) kernel is compiled for: 6 caps it at 80 VGPRs
 #ifndef MF_EMA_WPE
-#define MF_EMA_WPE 6
+#define MF_EMA_WPE 8
 #endif
 constexpr int EMA_E = 3;  // state elements per thread: F P K <= EMA_E x threads (host-checked)
 
@@ -378,7 +384,10 @@ struct MfTabs {
 //   prep (rolling_buffer.c:64-66, buffer.c:13-16, buffer.c:4-11), the prepared
 //   rows' sums for the offset correction, and the offset form, stored once.
 // CH: chunks per thread (>= ceil(F*M*N/8 / threads), host-checked).
-template <bool PREPARED, int CH>
+// WS: the workgroup's thread count is a multiple of the chunks per row, so
+// every chunk of a thread sits at the same row offset and reads the same
+// window chunk: one window load per thread (8 registers fewer per chunk)
+template <bool PREPARED, int CH, bool WS = false>
 __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm, char *smem, const MfTabs &tb,
                                          const int16_t *__restrict__ frames, int64_t f0, int nf)
 {
@@ -388,12 +397,19 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
     const int cpr = kp.N / 8;  // 16-byte chunks per row
     const int nchunk = rows * cpr;
     const int width = cpr < 64 ? cpr : 64;  // lanes of one wave that share a row
-    uint4 v[CH], w[CH];
+    constexpr int CW = WS ? 1 : CH;  // window chunks held per thread
+    uint4 v[CH], w[CW];
+    if constexpr (WS) {
+        w[0] = make_uint4(0, 0, 0, 0);
+        if (!PREPARED)
+            w[0] = reinterpret_cast<const uint4 *>(kp.window)[tid % cpr];
+    }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
         const int c = tid + nt * i;
         v[i] = make_uint4(0, 0, 0, 0);
-        w[i] = make_uint4(0, 0, 0, 0);
+        if constexpr (!WS)
+            w[i] = make_uint4(0, 0, 0, 0);
         if (c < nchunk) {
             const int r = c / cpr, k = c - r * cpr;
             if (kp.frame_ring) {  // streaming batch: frame f0 + r / M from its stream's ring
@@ -404,8 +420,9 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
             } else {
                 v[i] = reinterpret_cast<const uint4 *>(frames + f0 * kp.M * kp.N)[c];
             }
-            if (!PREPARED)
-                w[i] = reinterpret_cast<const uint4 *>(kp.window)[k];
+            if constexpr (!WS)
+                if (!PREPARED)
+                    w[i] = reinterpret_cast<const uint4 *>(kp.window)[k];
         }
     }
     // the prior: requested now, written once the frames have arrived
@@ -457,10 +474,11 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
             if (!PREPARED) {
                 // floor mean: int64 `total >> BITS` == int32 arithmetic shift here
                 const uint32_t off16 = (uint32_t)(sm.sums[r] >> kp.log2N) & 0xFFFFu;
-                x.x = prep_word(x.x, off16, w[i].x);
-                x.y = prep_word(x.y, off16, w[i].y);
-                x.z = prep_word(x.z, off16, w[i].z);
-                x.w = prep_word(x.w, off16, w[i].w);
+                const uint4 wi = w[WS ? 0 : i];
+                x.x = prep_word(x.x, off16, wi.x);
+                x.y = prep_word(x.y, off16, wi.y);
+                x.z = prep_word(x.z, off16, wi.z);
+                x.w = prep_word(x.w, off16, wi.w);
             }
             const int ps = ok ? sum_word(x.x) + sum_word(x.y) + sum_word(x.z) + sum_word(x.w) : 0;
             const int s = wsum(ps);
@@ -536,7 +554,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     EmaPre epre{};
     if constexpr (EMA)
         epre = ema_prefetch(kp, ef.sp, f0, nf);
-    stage_mf<PREPARED, CH>(kp, sm, smem, tb, frames, f0, nf);
+    stage_mf<PREPARED, CH, EMA>(kp, sm, smem, tb, frames, f0, nf);  // EMA launches: threads % (N / 8) == 0
     DIAG_STAMP(1);
     DIAG_STAMP(2);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
@@ -864,7 +882,8 @@ bool tdoa_direct_ema_fits(const tdoa_kparams &kp)
         return false;
     int F, threads, chunks;
     mf_shape(kp, F, threads, chunks, true);
-    return chunks <= 8 && F * kp.P * kp.K <= EMA_E * threads;
+    // (threads a multiple of the row's chunks: stage_mf's shared window chunk)
+    return chunks <= 8 && F * kp.P * kp.K <= EMA_E * threads && threads % (kp.N / 8) == 0;
 }
 
 int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const int16_t *frames,
@@ -907,7 +926,7 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         const tdoa_stream_fuse ef = ema ? *ema : tdoa_stream_fuse{};
         if (ema && (!count_dev || prepared))
             return tdoa_set_error(-1, "DIRECT: the EMA launch takes a device-sized batch of raw frames");
-        if (ema && kp.F * kp.P * kp.K > EMA_E * threads)
+        if (ema && (kp.F * kp.P * kp.K > EMA_E * threads || threads % (kp.N / 8) != 0))
             return tdoa_set_error(-1, "DIRECT: EMA state of a workgroup exceeds its prefetch registers");
 #define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                          \
     do {                                                                                                       \
@@ -922,6 +941,8 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
     do {                                  \
         if (chunks <= 2)                  \
             TDOA_LAUNCH_MF(PREP, TWC, 2); \
+        else if (chunks == 3)             \
+            TDOA_LAUNCH_MF(PREP, TWC, 3); \
         else if (chunks <= 4)             \
             TDOA_LAUNCH_MF(PREP, TWC, 4); \
         else                              \

@@ -733,9 +733,13 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
 
 bool tdoa_phat_r16_peak3(const tdoa_kparams &kp);
 
+bool tdoa_frame16_fused_grid(const tdoa_kparams &kp);
 // the launch solves the grid itself (no weighted-score scratch, no grid launch)
 bool tdoa_gcc_phat_grid_in_kernel(const tdoa_kparams &kp)
 {
+    const PhatRoute r = phat_route(kp);
+    if (r == PhatRoute::R16)
+        return tdoa_frame16_fused_grid(kp);
     return !tdoa_gcc_phat_needs_split(kp.M, kp.N) && tdoa_gcc_phat_fused_grid(kp);
 }
 

@@ -114,6 +114,15 @@ struct tdoa_kparams {
     uint16_t wc_off[TDOA_MAX_PAIRS];
     uint8_t wc_lo[TDOA_MAX_PAIRS], wc_w[TDOA_MAX_PAIRS];
     const uint32_t *wc_chunks;
+    // the grid solve fused into k_frame16 (tdoa_phat_r16.hip, "FG"): every
+    // (entry, pair) range of the k_grid_bb tables as a query into sparse-table
+    // levels of the compact layout above: e | lv << 11 | d << 13 with e =
+    // wc_off[p] + lo - wc_lo[p] the first window's element of level lv
+    // (2^lv <= n = hi - lo + 1 < 2^(lv+1); level 0 = the scores) and d = n - 2^lv
+    // the second window's distance; rows of 32 (P <= 28 used)
+    const uint16_t *fg_q;      // [bb_NT][32]
+    const uint16_t *fg_tup;    // [U][32] the regrouped tuples as compact element indices (wc_off + lag - wc_lo)
+    int32_t fg_ok;             // the tables exist (n <= 15, wc_CK <= 2048, bb_NT <= 256, P <= 32)
     // DIRECT on the streaming batch read straight from the capture ring (the
     // persistent trigger lists the firing streams and copies nothing): frame f
     // of the batch is stream frame_ids[f]'s samples from ring index

@@ -757,7 +757,7 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
                                                  const int (&p)[NP], const bool (&on)[NP], int ka, int kb,
                                                  bool oka, bool okb, const float (&sa)[NP], const float (&sb)[NP],
                                                  bool lane0, const int (&wlo)[NP], const int (&ww)[NP],
-                                                 const int (&woff)[NP])
+                                                 const int (&woff)[NP], float *wl = nullptr)
 {
     const int K = kp.K, S = kp.S;
     int bkey[NP], bk[NP];
@@ -790,6 +790,7 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
         const int b = bk[h] < 0 ? 0 : (bk[h] >= K ? K - 1 : bk[h]);  // NaN scores: keep the index in range
         const size_t gb = (size_t)(fr * P + p[h]) * K;
         float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + woff[h] - wlo[h] : nullptr;
+        float *wlp = wl ? wl + woff[h] - wlo[h] : nullptr;  // FG: the frame's compact scores in LDS
         if (oka) {
             const int dd = ka > b ? ka - b : b - ka;
             const float wa = sa[h] * priorl[dd];
@@ -799,6 +800,8 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
                 out.weighted_f[gb + ka] = wa;
             if (wcp && ka >= wlo[h] && ka < wlo[h] + ww[h])
                 wcp[ka] = wa;
+            if (wlp && ka >= wlo[h] && ka < wlo[h] + ww[h])
+                wlp[ka] = wa;
         }
         if (okb) {
             const int dd = kb > b ? kb - b : b - kb;
@@ -809,6 +812,8 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
                 out.weighted_f[gb + kb] = wb;
             if (wcp && kb >= wlo[h] && kb < wlo[h] + ww[h])
                 wcp[kb] = wb;
+            if (wlp && kb >= wlo[h] && kb < wlo[h] + ww[h])
+                wlp[kb] = wb;
         }
         if (pk3) {
             // the least-squares refinement's raw scores around the peak: the
@@ -826,6 +831,214 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
     }
 }
 
+// ---- the grid solve fused into k_frame16 (FG; vga_heatmap.h:99-108, the
+// exact branch and bound of tdoa_grid_bb.h spread over waves).  The last pair
+// round leaves groups idle (config 4: pairs 24-27 on 4 of 8 groups; config 3:
+// pairs 4-5 on 2 of 4); their NGW = 8 waves solve the PREVIOUS frame's grid
+// between the round's barriers, from that frame's weighted scores kept in LDS
+// in the compact layout (kp.wc_*), while the busy groups run the round's
+// passes.  Segments (one per barrier interval of the round):
+//   A  sparse-table levels S_lv[i] = max w[i .. i + 2^lv - 1], lv = 1..3, of the
+//      compact array (lane: 8 elements from 15 reads), into the idle groups'
+//      transform buffers; the entries' query rows (kp.fg_q) requested
+//   B  every entry's bound: sum over pairs, in L's own pair order from 0, of
+//      the range maximum max(S_lv[e], S_lv[e + d]) -- >= the float L of every
+//      tuple of the entry (float addition is monotone in each operand)
+//   C  wave gw takes the largest bound among the entries t = gw mod NGW (first
+//      on ties, NaN never) and evaluates it: its <= 64 tuples, one per lane,
+//      L = 0 + w_0[l_0] + w_1[l_1] + ... (the exhaustive scan's association),
+//      (max L, smallest first-cell index) by a 64-bit key
+//   D  the wave's key and candidate to LDS
+//   E  best8 = the best of the NGW keys; each wave then evaluates, in entry
+//      order, every entry of its partition other than its candidate whose
+//      bound is not below the best so far (NaN bounds included) -- an entry
+//      below it cannot hold the maximum -- and stores its key
+// and after the round's closing barrier one lane takes the best of the NGW
+// final keys: cell, max_Lf, (x, y) of k_grid_bb, bit for bit (ties: the
+// smallest first-cell tuple; no L above -inf: tuple 0 and -inf).  The last
+// frame of a workgroup is solved the same way after the frame loop.
+constexpr int FG_NGW = 8;  // grid waves
+struct FgLds {
+    float *w;        // [2][CKp] compact weighted scores (DM 0: by frame parity; DM 1: [0] only)
+    float *bnd;      // [256] entry bounds
+    uint64_t *key;   // [NGW] seg C keys, then [NGW] seg E keys
+    int *cand;       // [NGW] seg C candidates
+};
+__device__ __forceinline__ uint64_t fg_key(float L, int ui)
+{
+    if (!(L > -INFINITY))  // the exhaustive scan records only L above its start value
+        return 0;
+    return ((uint64_t)((uint32_t)fkey(L) ^ 0x80000000u) << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)ui);
+}
+__device__ __forceinline__ float fg_key_value(uint64_t k)
+{
+    return k ? fkey_value((int)((uint32_t)(k >> 32) ^ 0x80000000u)) : -INFINITY;
+}
+__device__ __forceinline__ uint64_t fg_wave_max(uint64_t k) { return lane63_u64(wave_umax_dpp(k)); }
+
+// kp's fields through an opaque kernarg pointer (kernarg_base): loaded where the
+// segment uses them (scalar loads) instead of hoisted to the kernel's start and
+// held in scalar registers across the frame loop (they spilled)
+__device__ __forceinline__ const __attribute__((address_space(4))) tdoa_kparams *kernarg_kp()
+{
+    return reinterpret_cast<const __attribute__((address_space(4))) tdoa_kparams *>(kernarg_base());
+}
+template <int P>
+struct FgGrid {
+    FgLds L;
+    float *lvl;  // [3][LV] levels (the idle groups' buffers), LV = CK rounded to 8
+    int CK, CKp;
+    __device__ __forceinline__ int LV() const { return (CK + 7) & ~7; }  // a lane writes 8 elements per level
+    // seg A: levels of the compact array w; prefetch of the bound rows
+    __device__ __forceinline__ void levels(const float *w, int gw, int lane, uint4 (&qr)[4]) const
+    {
+        const auto *kp = kernarg_kp();
+        const int t = gw * 64 + lane;
+        const uint4 *row = reinterpret_cast<const uint4 *>(kp->fg_q + (size_t)(t < kp->bb_NT ? t : 0) * 32);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            qr[i] = row[i];
+        for (int i0 = 8 * t; i0 < CK; i0 += 8 * 64 * FG_NGW) {
+            float x[15];
+#pragma unroll
+            for (int d = 0; d < 15; d++)
+                x[d] = w[i0 + d < CK ? i0 + d : CK - 1];
+#pragma unroll
+            for (int d = 0; d < 14; d++)
+                x[d] = fmaxf(x[d], x[d + 1]);
+            float4 *d1 = reinterpret_cast<float4 *>(lvl + i0);
+            d1[0] = make_float4(x[0], x[1], x[2], x[3]);
+            d1[1] = make_float4(x[4], x[5], x[6], x[7]);
+#pragma unroll
+            for (int d = 0; d < 12; d++)
+                x[d] = fmaxf(x[d], x[d + 2]);
+            float4 *d2 = reinterpret_cast<float4 *>(lvl + LV() + i0);
+            d2[0] = make_float4(x[0], x[1], x[2], x[3]);
+            d2[1] = make_float4(x[4], x[5], x[6], x[7]);
+#pragma unroll
+            for (int d = 0; d < 8; d++)
+                x[d] = fmaxf(x[d], x[d + 4]);
+            float4 *d3 = reinterpret_cast<float4 *>(lvl + 2 * LV() + i0);
+            d3[0] = make_float4(x[0], x[1], x[2], x[3]);
+            d3[1] = make_float4(x[4], x[5], x[6], x[7]);
+        }
+    }
+    // seg B: the bounds of entries gw * 64 + lane
+    __device__ __forceinline__ void bounds(const float *w, int gw, int lane, const uint4 (&qr)[4]) const
+    {
+        const int t = gw * 64 + lane;
+        if (t >= kernarg_kp()->bb_NT)
+            return;
+        uint32_t qw[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            qw[4 * i] = qr[i].x;
+            qw[4 * i + 1] = qr[i].y;
+            qw[4 * i + 2] = qr[i].z;
+            qw[4 * i + 3] = qr[i].w;
+        }
+        float mp[P];
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            const uint32_t q = (qw[p >> 1] >> (16 * (p & 1))) & 0xFFFFu;
+            const int e = (int)(q & 2047u), lv = (int)((q >> 11) & 3u), dd = (int)(q >> 13);
+            const float *base = lv ? lvl + (lv - 1) * LV() : w;
+            mp[p] = fmaxf(base[e], base[e + dd]);
+        }
+        float b = 0.0f;
+#pragma unroll
+        for (int p = 0; p < P; p++)  // in L's own pair order, from 0
+            b += mp[p];
+        L.bnd[t] = b;
+    }
+    // one entry's tuples, one per lane: the wave's best key.  The tuples come as
+    // compact element indices (kp.fg_tup: no per-pair offsets in scalar registers)
+    __device__ __forceinline__ uint64_t evaluate(const float *w, int c, int lane) const
+    {
+        constexpr int NQ = (P + 7) / 8;  // 16-B loads of 8 indices
+        const auto *kp = kernarg_kp();
+        const int start = kp->bb_tile[2 * c], cnt = kp->bb_tile[2 * c + 1];
+        uint64_t k = 0;
+        if (lane < cnt) {
+            const int u = start + lane;
+            const uint4 *row = reinterpret_cast<const uint4 *>(kp->fg_tup + (size_t)u * 32);
+            uint4 q[NQ];
+#pragma unroll
+            for (int i = 0; i < NQ; i++)
+                q[i] = row[i];
+            const int ui = kp->bb_uidx[u];
+            float Lv = 0.0f;
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                const uint4 &qq = q[p >> 3];
+                const uint32_t wd = ((p >> 1) & 3) == 0 ? qq.x : (((p >> 1) & 3) == 1 ? qq.y : (((p >> 1) & 3) == 2 ? qq.z : qq.w));
+                Lv += w[(wd >> (16 * (p & 1))) & 0xFFFFu];
+            }
+            k = fg_key(Lv, ui);
+        }
+        return fg_wave_max(k);
+    }
+    // seg C: the partition's best-bound entry, evaluated
+    __device__ __forceinline__ uint64_t candidate(const float *w, int gw, int lane, int &cand) const
+    {
+        const int t = gw + FG_NGW * lane;
+        uint64_t bk = 0;
+        if (t < kernarg_kp()->bb_NT) {
+            const float b = L.bnd[t];
+            if (b == b)  // NaN bounds never seed (k_grid_bb)
+                bk = ((uint64_t)((uint32_t)fkey(b) ^ 0x80000000u) << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)t);
+        }
+        bk = fg_wave_max(bk);
+        cand = bk ? (int)(0xFFFFFFFFu - (uint32_t)bk) : -1;
+        return cand >= 0 ? evaluate(w, cand, lane) : 0;
+    }
+    // seg E: best8, then the partition's other entries not below the best
+    __device__ __forceinline__ uint64_t rest(const float *w, int gw, int lane) const
+    {
+        uint64_t best = 0;
+#pragma unroll
+        for (int i = 0; i < FG_NGW; i++)
+            best = L.key[i] > best ? L.key[i] : best;
+        const int mine = L.cand[gw];
+        const int t = gw + FG_NGW * lane;
+        const float bl = fg_key_value(best);
+        const bool need = t < kernarg_kp()->bb_NT && t != mine && !(L.bnd[t] < bl);
+        uint64_t m = __ballot(need);
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const int c = gw + FG_NGW * j;
+            if (L.bnd[c] < fg_key_value(best))  // the best may have risen since
+                continue;
+            const uint64_t k = evaluate(w, c, lane);
+            best = k > best ? k : best;
+        }
+        return best;
+    }
+    // after the closing barrier: the frame's outputs (one lane)
+    __device__ __forceinline__ void finish(int64_t f) const
+    {
+        const auto *kp = kernarg_kp();
+        const auto *out = kernarg_out();
+        uint64_t best = 0;
+#pragma unroll
+        for (int i = 0; i < FG_NGW; i++)
+            best = L.key[FG_NGW + i] > best ? L.key[FG_NGW + i] : best;
+        int ui = best ? (int)(0xFFFFFFFFu - (uint32_t)best) : 0;
+        ui = (ui < 0 || ui >= kp->U) ? 0 : ui;  // no L above -inf: tuple 0 (k_grid_bb)
+        const int cell = kp->tuple_cell[ui];
+        if (int32_t *oc = out->cell)
+            oc[f] = cell;
+        if (float *om = out->max_Lf)
+            om[f] = fg_key_value(best);
+        if (float *oxy = out->xy) {
+            const int W = kp->grid_W, cx = cell % W, cy = cell / W;
+            oxy[2 * f] = (float)(cx - kp->half_w) / kp->grid_scale;
+            oxy[2 * f + 1] = (float)(kp->half_h - cy) / kp->grid_scale;
+        }
+    }
+};
+
 // (kp, out) must stay the first two parameters: kernarg_out() reads `out`
 // at its kernarg offset
 // DM (deferred outputs): 0 -- every round's pass 3 runs its pair's argmax and
@@ -835,7 +1048,7 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
 // wave per pair in parallel.  (Running the earlier rounds' epilogue on the
 // last round's idle groups instead measured slower at config 3: 3.865 vs
 // 3.826 ms per step.)
-template <int C, int M, int DM, bool XS = (F16_XS != 0)>
+template <int C, int M, int DM, bool XS = (F16_XS != 0), bool FG = false>
 __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout out,
                                                      const int16_t *__restrict__ frames, int64_t B,
                                                      float e2)
@@ -856,6 +1069,23 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     f2 *tw3 = (f2 *)(priorl + 128);  // [R1][64] pass-3 twiddles per lane (row 0 unused)
     uint32_t *winl = (uint32_t *)(tw3 + R1 * 64);  // f16_win_lds: [C / 2] window words
     float *scl = (float *)(winl + (f16_win_lds<C>() ? C / 2 : 0));  // DM 1: [P][K] raw scores of the frame
+    // FG: the fused grid's LDS (FgLds) after scl, 16-B aligned; its levels in
+    // the last round's idle groups' buffers
+    constexpr int GI0 = P - (ROUNDS - 1) * G;  // first idle group of the last round
+    static_assert(!FG || (G - GI0) * (T / 64) >= FG_NGW, "the last round must leave FG_NGW idle waves");
+    const int CKp = (kp.wc_CK + 3) & ~3;
+    FgLds fgl{};
+    if constexpr (FG) {
+        const int fo = (int)(((char *)(scl + (DM == 1 ? P * kp.K : 0)) - smem + 15) & ~15);
+        fgl.w = (float *)(smem + fo);
+        fgl.bnd = fgl.w + 2 * CKp;
+        fgl.key = (uint64_t *)(fgl.bnd + 256);
+        fgl.cand = (int *)(fgl.key + 2 * FG_NGW);
+    }
+    const FgGrid<P> fgg{fgl, (float *)(bufs + GI0 * BUF), kp.wc_CK, CKp};
+    int64_t prev = -1;  // FG: the previous frame of this workgroup (its grid is still to solve)
+    int fpar = 0;       // FG, DM 0: this iteration's half of the double-buffered scores (by iteration, not
+                        // frame parity: a workgroup's frames are gridDim.x apart)
     const int g = (int)threadIdx.x / T;
     const int K = kp.K, S = kp.S;
     f2 *buf = bufs + g * BUF;
@@ -973,6 +1203,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // thread indices the compiler cannot prove loop-invariant: the passes'
     // twiddle reads stay in the body instead of being hoisted (and spilled)
     const int tid = opaque_idx((int)threadIdx.x), j = tid - g * T, pj = pidx(j);
+    // FG: this frame's compact scores go to fgw, the previous frame's are at pgw
+    float *fgw = FG ? fgl.w + (DM == 0 ? fpar * CKp : 0) : nullptr;
+    const float *pgw = FG ? fgl.w + (DM == 0 ? (fpar ^ 1) * CKp : 0) : nullptr;
+    const bool fgr = FG && prev >= 0 && kp.fg_ok == 1;  // (fg_ok 2: TDOA_F16_FG=skip, A/B of the bare structure)
     if (fr == diag_fr) {
 #ifdef TDOA_DIAG
         stamp[30] = __builtin_amdgcn_s_memrealtime();
@@ -1083,6 +1317,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 v[r] = F16_LD(buf + (XS ? cjl.at(r) : pjl + po(T * r)));
             dftp<16, true, false>(v);
         }
+        // FG, last round: the idle groups' waves solve the previous frame's grid
+        constexpr bool FGL = FG && decltype(rc)::value == ROUNDS - 1;
+        const int gw = (tl - GI0 * T) >> 6, gln = tl & 63;
+        uint4 fqr[4];
+        if constexpr (FGL) {
+            if (!on && fgr)
+                fgg.levels(pgw, gw, gln, fqr);  // seg A
+        }
         __syncthreads();
         if (fr == diag_fr)
             F16_MARK();
@@ -1091,6 +1333,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 buf[XS ? (b1 ^ r) : 17 * jl + r] = v[brev<16>(r)];
+        }
+        if constexpr (FGL) {
+            if (!on && fgr)
+                fgg.bounds(pgw, gw, gln, fqr);  // seg B
         }
         __syncthreads();
         if (fr == diag_fr)
@@ -1117,6 +1363,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             x15 = x15 + (r ? dif_tw<false>(d0, d1, 4 * r) : d0 - d1);
         }
 #undef F16_TW256
+        uint64_t fgk = 0;
+        int fgc = -1;
+        if constexpr (FGL) {
+            if (!on && fgr)
+                fgk = fgg.candidate(pgw, gw, gln, fgc);  // seg C
+        }
         __syncthreads();
         if (fr == diag_fr)
             F16_MARK();
@@ -1128,6 +1380,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             buf[XS ? o ^ 17 : o + 17] = x1;
             buf[XS ? o ^ 34 : o + 34] = x14;
             buf[XS ? o ^ 51 : o + 51] = x15;
+        }
+        if constexpr (FGL) {
+            if (!on && fgr && gln == 0) {  // seg D
+                fgl.key[gw] = fgk;
+                fgl.cand[gw] = fgc;
+            }
         }
         __syncthreads();
         if (fr == diag_fr)
@@ -1173,13 +1431,24 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 const bool on1[1] = {true};
                 const float a1[1] = {sa}, b1[1] = {sb};
                 frame16_pair_out<1>(kp, out, priorl, lagl, fr, P, pp, on1, ka, kb, oka, okb, a1, b1, l == 0, lo, wd,
-                                    of);
+                                    of, fgw);
+            }
+        }
+        if constexpr (FGL) {
+            if (!on && fgr) {  // seg E
+                const uint64_t kk = fgg.rest(pgw, gw, gln);
+                if (gln == 0)
+                    fgl.key[FG_NGW + gw] = kk;
             }
         }
         __syncthreads();  // the buffers are rewritten by the next round
         if (fr == diag_fr)
             F16_MARK();
     });
+    if constexpr (FG) {
+        if (fgr && tid == 0)
+            fgg.finish(prev);  // the previous frame's cell, max L, (x, y)
+    }
     if constexpr (DM == 1) {
         // every pair's argmax and outputs, wave w: pairs w, w + 16 (lane l:
         // lags l and l + 64, K <= 127)
@@ -1197,7 +1466,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         pin_words();
         if (on2[0])
             frame16_pair_out<2>(kp, out, priorl, lagl, fr, P, pp, on2, ln, ln + 64, oka, okb, sa, sb, ln == 0, ep_lo,
-                                ep_w, ep_off);
+                                ep_w, ep_off, fgw);
         __syncthreads();  // lagl complete for the gate; scl free for the next frame
         if (fr == diag_fr)
             F16_MARK();
@@ -1209,6 +1478,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             tot += lagl[q] * lagl[q];
         out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
     }
+    prev = fr;
+    fpar ^= 1;
 #ifdef TDOA_DIAG
     if (fr == diag_fr) {
         stamp[31] = __builtin_amdgcn_s_memrealtime();
@@ -1216,6 +1487,39 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 #endif
     }  // frames
+    if constexpr (FG) {
+        // the last frame's grid, by waves 0 .. FG_NGW - 1 (every buffer is free)
+        if (prev >= 0 && kp.fg_ok == 1) {
+            const int tid = (int)threadIdx.x, gw = tid >> 6, gln = tid & 63;
+            const bool act = gw < FG_NGW;
+            const float *pgw = fgl.w + (DM == 0 ? (fpar ^ 1) * CKp : 0);  // (fpar toggled after the last frame)
+            uint4 fqr[4];
+            __syncthreads();  // the last frame's scores are in LDS
+            if (act)
+                fgg.levels(pgw, gw, gln, fqr);
+            __syncthreads();
+            if (act)
+                fgg.bounds(pgw, gw, gln, fqr);
+            __syncthreads();
+            int fgc = -1;
+            uint64_t fgk = 0;
+            if (act)
+                fgk = fgg.candidate(pgw, gw, gln, fgc);
+            if (act && gln == 0) {
+                fgl.key[gw] = fgk;
+                fgl.cand[gw] = fgc;
+            }
+            __syncthreads();
+            if (act) {
+                const uint64_t kk = fgg.rest(pgw, gw, gln);
+                if (gln == 0)
+                    fgl.key[FG_NGW + gw] = kk;
+            }
+            __syncthreads();
+            if (tid == 0)
+                fgg.finish(prev);
+        }
+    }
 #ifdef TDOA_DIAG
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 128)
         for (int i = 0; i < 32; i++)
@@ -1224,12 +1528,37 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 }
 #undef F16_MARK
 
+// the fused grid (FG) applies: the last pair round leaves FG_NGW idle waves,
+// the tables exist, TDOA_F16_FG is not "0", and the LDS fits (with the
+// deferred scores where the launch defers)
 template <int C, int M>
-int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
-                   float e2, hipStream_t st)
+constexpr bool fg_shape()
 {
-    if (B <= 0)
-        return 0;
+    constexpr int G = 16384 / C, P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G, GI0 = P - (ROUNDS - 1) * G;
+    return (G - GI0) * (C / 16 / 64) >= FG_NGW;
+}
+// TDOA_F16_FG: 1 on, 0 off, skip (A/B of the bare FG structure); unset: on
+// with the deferred epilogue only (config 4: time-neutral, 92.98 vs 93.04 ms per
+// step, and no weighted-score round trip through HBM), off with in-round
+// outputs (config 3: 4.04 vs 3.50 ms -- its k_grid_bb is cheap)
+static int fg_mode()
+{
+    static const int m = [] {
+        const char *e = getenv("TDOA_F16_FG");
+        if (!e)
+            return -1;
+        return !strcmp(e, "1") ? 1 : (!strcmp(e, "skip") ? 2 : 0);
+    }();
+    return m;
+}
+static size_t fg_lds_bytes(const tdoa_kparams &kp)
+{
+    const size_t CKp = (size_t)((kp.wc_CK + 3) & ~3);
+    return 16 + 2 * CKp * 4 + 256 * 4 + 2 * FG_NGW * 8 + FG_NGW * 4;
+}
+template <int C, int M>
+static bool frame16_defer(const tdoa_kparams &kp)
+{
     // deferred pair outputs (DM 1) at three or more pair rounds when the
     // frame's [P][K] scores fit next to the buffers (config 4: 10.4 KiB of 13.3
     // free; 98.5 vs 104.4 ms per step; config 3, two rounds: 3.87 vs 3.83 ms)
@@ -1240,17 +1569,62 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
         return e ? atoi(e) : -1;
     }();
     const size_t lds_defer = frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float);
-    const bool defer = (force >= 0 ? force == 1 : ROUNDS >= 3) && lds_defer <= 160 * 1024;
-    const void *fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
-    const size_t lds = defer ? lds_defer : frame16_lds_base<C>();
+    return (force >= 0 ? force == 1 : ROUNDS >= 3) && lds_defer <= 160 * 1024;
+}
+template <int C, int M>
+static bool frame16_fg(const tdoa_kparams &kp)
+{
+    if (!fg_shape<C, M>() || !kp.fg_ok || !kp.fg_q || !kp.fg_tup || fg_mode() == 0 || kp.P != M * (M - 1) / 2)
+        return false;
+    const bool defer = frame16_defer<C, M>(kp);
+    if (fg_mode() < 0 && !defer)
+        return false;
+    const size_t base = frame16_lds_base<C>() + (defer ? (size_t)kp.P * kp.K * sizeof(float) : 0);
+    return base + fg_lds_bytes(kp) <= 160 * 1024;
+}
+
+template <int C, int M>
+int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
+                   float e2, hipStream_t st)
+{
+    if (B <= 0)
+        return 0;
+    constexpr int P = M * (M - 1) / 2;
+    const bool defer = frame16_defer<C, M>(kp);
+    // the grid solved in the kernel when the caller asks for it (FG)
+    const bool fg = frame16_fg<C, M>(kp) && (out.cell || out.xy || out.max_Lf);
+    const void *fn;
+    if constexpr (fg_shape<C, M>())
+        fn = defer ? (fg ? (const void *)k_frame16<C, M, 1, F16_XS != 0, true> : (const void *)k_frame16<C, M, 1>)
+                   : (fg ? (const void *)k_frame16<C, M, 0, F16_XS != 0, true> : (const void *)k_frame16<C, M, 0>);
+    else
+        fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
+    const size_t lds =
+        (defer ? frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float) : frame16_lds_base<C>()) +
+        (fg ? fg_lds_bytes(kp) : 0);
+    tdoa_kparams kpl = kp;
+    if (fg && fg_mode() == 2)
+        kpl.fg_ok = 2;  // A/B only: the FG kernel without its grid work (no grid outputs)
     const int res = tdoa_resident_blocks(fn, 1024, lds);
     if (res < 1)
         return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
     const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
-    if (defer)
-        hipLaunchKernelGGL((k_frame16<C, M, 1>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
-    else
-        hipLaunchKernelGGL((k_frame16<C, M, 0>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+    if constexpr (fg_shape<C, M>()) {
+        if (fg) {
+            if (defer)
+                hipLaunchKernelGGL((k_frame16<C, M, 1, F16_XS != 0, true>), dim3((unsigned)grid), dim3(1024), lds, st,
+                                   kpl, out, frames, B, e2);
+            else
+                hipLaunchKernelGGL((k_frame16<C, M, 0, F16_XS != 0, true>), dim3((unsigned)grid), dim3(1024), lds, st,
+                                   kpl, out, frames, B, e2);
+        }
+    }
+    if (!fg) {
+        if (defer)
+            hipLaunchKernelGGL((k_frame16<C, M, 1>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+        else
+            hipLaunchKernelGGL((k_frame16<C, M, 0>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];
@@ -1665,6 +2039,23 @@ bool frame16w_pick()
 bool frame16_shape(const tdoa_kparams &kp)
 {
     return (kp.N == 4096 && (kp.M == 3 || kp.M == 4)) || (kp.N == 2048 && (kp.M == 4 || kp.M == 8));
+}
+bool tdoa_phat_r16_fits(int M, int N, int S);
+// a grid-requesting launch of this shape solves the grid in k_frame16 (FG):
+// no weighted-score scratch and no k_grid_bb launch (tdoa_capi.cpp run_batch)
+bool tdoa_frame16_fused_grid(const tdoa_kparams &kp)
+{
+    if (!tdoa_phat_r16_fits(kp.M, kp.N, kp.S) || !frame16_shape(kp))
+        return false;
+    if (kp.N == 2048 && kp.M == 8)
+        return !frame16w_pick() && frame16_fg<2048, 8>(kp);
+    if (kp.N == 4096 && kp.M == 4)
+        return frame16_fg<4096, 4>(kp);
+    if (kp.N == 4096 && kp.M == 3)
+        return frame16_fg<4096, 3>(kp);
+    if (kp.N == 2048 && kp.M == 4)
+        return frame16_fg<2048, 4>(kp);
+    return false;
 }
 // the name of the fused kernel a frame16_shape launch runs
 const char *frame16_kernel_name(const tdoa_kparams &kp)

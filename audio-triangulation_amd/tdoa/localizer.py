@@ -102,6 +102,10 @@ class Localizer:
         """Name of the kernel a batch of this context runs first (tdoa_batch_kernel)."""
         return (load().tdoa_batch_kernel(self._ctx) or b"").decode()
 
+    def batch_grid_fused(self) -> bool:
+        """A grid-requesting batch solves the grid inside its first kernel (tdoa_batch_grid_fused)."""
+        return bool(load().tdoa_batch_grid_fused(self._ctx))
+
     def window(self) -> np.ndarray:
         w = np.zeros(self.dims.N, np.int32)
         check(load().tdoa_get_window(self._ctx, w.ctypes.data_as(C.c_void_p)), "tdoa_get_window")

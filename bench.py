@@ -44,15 +44,17 @@ import torch  # noqa: E402
 from tdoa import shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-CALIB_JSON = os.path.join(ROOT, "profiles", "r04_hbm_calibration.json")
+CALIB_JSON = os.path.join(ROOT, "profiles", "r05_hbm_calibration.json")
 
 
 def achievable_hbm():
     """Measured achievable HBM read rate (tools/hbm_copy.hip under rocprofv3,
-    profiles/r04_hbm_calibration.json): the denominator of frac_achievable."""
+    profiles/r05_hbm_calibration.json): the denominator of frac_achievable; and the
+    faster of its two copies (nontemporal / default-policy stores), read + write."""
     try:
         c = json.load(open(CALIB_JSON))
-        return float(c["read_gbs_rocprof"]), float(c["copy_gbs_rocprof"])
+        cp = max(float(c.get("copy_gbs_rocprof", 0)), float(c.get("copy_plain_gbs_rocprof", 0)))
+        return float(c["read_gbs_rocprof"]), cp
     except (OSError, ValueError, KeyError):
         return None, None
 
@@ -80,13 +82,14 @@ CONFIGS = {
 }
 
 
-def dominant_kernel(config: int, engine: str, first: str = "") -> str:
+def dominant_kernel(config: int, engine: str, first: str = "", fused: bool = True) -> str:
     """Name of the kernel(s) a launch runs (the ones `traffic` was measured on);
-    `first` is the library's own answer (Localizer.batch_kernel)."""
+    `first` is the library's own answer (Localizer.batch_kernel), `fused` whether
+    the grid is solved inside it (Localizer.batch_grid_fused)."""
     if config == 2:
         return first or ("k_p1k_lean" if engine == "gcc_phat" else "k_direct_mfma")
     if config in (3, 4) and engine == "gcc_phat":
-        return "k_frame16 + k_grid_bb"
+        return "k_frame16" if fused else "k_frame16 + k_grid_bb"
     return ""
 
 
@@ -260,6 +263,7 @@ def time_engine(engine, args, dev, ri, cache):
     res = {
         "engine": engine,
         "kernel": loc.batch_kernel(),
+        "grid_fused": loc.batch_grid_fused(),
         "value": total / t["wall_max_s"],
         "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
         "kernel_ms": kern_s * 1e3,
@@ -539,10 +543,10 @@ def cpu_baseline(args, lut, window):
                       f"vga_heatmap.h algorithm, DIRECT integer xcorr), OpenMP {threads} threads"}
 
 
-def traffic_entry(args, first=""):
+def traffic_entry(args, first="", fused=True):
     """HBM bytes per launch from the committed PMC passes, used only when they
     were taken on the kernel this run dispatches."""
-    kname = dominant_kernel(args.config, args.engine, first)
+    kname = dominant_kernel(args.config, args.engine, first, fused)
     if not kname or not os.path.exists(args.traffic_json):
         return None, None
     try:
@@ -553,6 +557,8 @@ def traffic_entry(args, first=""):
     names = kname.split(" + ")
     if e.get("kernel") != names[0]:
         return None, None
+    if args.config in (3, 4) and fused and any(k.startswith("k_grid") for k in e.get("kernels", {})):
+        return None, None  # a pass taken with the separate grid kernel: not this launch's traffic
     src = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
            f"passes on {kname} ({e.get('date', 'undated')}), read = 2 x FETCH_SIZE")
     if len(names) == 1:
@@ -585,6 +591,23 @@ def stream_traffic(args):
                       "read = 2 x FETCH_SIZE; the trigger re-reads the two previous hops")
 
 
+def executed_flops(args, frames):
+    """FP32 flops a launch of this config actually executes: SQ_INSTS_VALU_FLOPS_FP32 per
+    dispatch (tools/summarize_flops.py -> profiles/valu_flops.json) per localization, times
+    this launch's frames; (flops per launch, source) or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "valu_flops.json")
+    try:
+        e = json.load(open(path)).get(f"c{args.config}_{args.engine}") or {}
+    except (OSError, ValueError):
+        return None, None
+    if not e.get("executed_fp32_flops_per_loc"):
+        return None, None
+    return e["executed_fp32_flops_per_loc"] * frames, (
+        f"profiles/valu_flops.json: rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 on the launch's kernels "
+        f"({e.get('date', 'undated')}), {e['executed_fp32_flops_per_loc']:.4g} flop per localization executed "
+        f"against the model's {e['survey_model_flops_per_loc']:.4g}")
+
+
 def _achievable(achieved_gbs):
     """frac against the measured achievable read rate beside the spec fraction."""
     rd, cp = achievable_hbm()
@@ -592,7 +615,7 @@ def _achievable(achieved_gbs):
         return {"achievable": None, "frac_achievable": None}
     return {"achievable": rd, "frac_achievable": achieved_gbs / rd,
             "achievable_source": f"{os.path.relpath(CALIB_JSON, ROOT)}: 16-B-per-lane read sweep over 1 GiB "
-                                 f"(rocprofv3 {rd:.0f} GB/s; copy {cp:.0f} GB/s read+write)"}
+                                 f"(rocprofv3 {rd:.0f} GB/s; the kernels are read-dominated)"}
 
 
 def launch_workers(args):
@@ -684,7 +707,7 @@ def main():
                             ri, cache)
     world = shard.ranks_seen()
     if ri.rank == 0:
-        traffic, tsrc = traffic_entry(args, main_res.get("kernel", ""))
+        traffic, tsrc = traffic_entry(args, main_res.get("kernel", ""), main_res.get("grid_fused", True))
         cfg = CONFIGS[args.config]
         shape = f"{cfg['M']}-mic x {cfg['N']}-sample frames"
         B = main_res["frames_per_rank"]
@@ -724,15 +747,13 @@ def main():
                          **_achievable(main_res["achieved_gbs"]),
                          "traffic": traffic,
                          "traffic_source": tsrc,
-                         "kernel": dominant_kernel(args.config, args.engine, main_res.get("kernel", ""))
+                         "kernel": dominant_kernel(args.config, args.engine, main_res.get("kernel", ""),
+                                                   main_res.get("grid_fused", True))
                          or "all kernels of a launch",
                          "kernel_ms": main_res["kernel_ms"],
                          "bytes_per_loc": main_res["bytes_per_loc"]},
             # the bound that actually binds an fp32 FFT path: FP32 vector issue
-            "valu_roofline": {"achieved": main_res["valu_tflops"], "peak": VALU_PEAK_TFLOPS,
-                              "unit": "TFLOP/s", "frac": main_res["valu_tflops"] / VALU_PEAK_TFLOPS,
-                              "flop_model": "SURVEY.md 8(d) GCC-PHAT model"}
-            if args.engine == "gcc_phat" else None,
+            "valu_roofline": _valu_roofline(args, main_res) if args.engine == "gcc_phat" else None,
             "parity": main_res.get("parity"),
             "cpu_baseline": None,
         }
@@ -743,6 +764,20 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args, cache["lut"], cache["window"])
         print(json.dumps(line), flush=True)
     shard.finalize()
+
+
+def _valu_roofline(args, res):
+    """FP32 VALU roofline of the launch: SURVEY.md 8(d)'s flop model (forward FFTs, PHAT
+    and FULL inverse FFTs per localization) and, where a counter pass exists for this
+    batch, the flops the kernels actually executed (the pruned inverse as built)."""
+    r = {"achieved": res["valu_tflops"], "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": res["valu_tflops"] / VALU_PEAK_TFLOPS, "flop_model": "SURVEY.md 8(d) GCC-PHAT model"}
+    fl, src = executed_flops(args, res["frames_per_rank"])
+    if fl:
+        t = fl / (res["kernel_ms"] * 1e-3) / 1e12
+        r["executed"] = {"achieved": t, "frac": t / VALU_PEAK_TFLOPS, "flops_per_launch": fl,
+                         "source": src}
+    return r
 
 
 def main_stream(args, dev, ri, cache):

@@ -215,6 +215,10 @@ int tdoa_abi_version(void);
 /* Name of the kernel a tdoa_localize_batch call of this context runs first
  * (diagnostics: profile and HBM-traffic attribution); "" if none applies. */
 const char *tdoa_batch_kernel(const tdoa_ctx *ctx);
+/* 1 if a grid-requesting tdoa_localize_batch of this context solves the grid
+ * inside that first kernel (no weighted-score scratch, no separate grid
+ * launch), 0 if a grid kernel follows it (diagnostics, like tdoa_batch_kernel). */
+int tdoa_batch_grid_fused(const tdoa_ctx *ctx);
 
 #ifdef __cplusplus
 }

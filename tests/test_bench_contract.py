@@ -47,16 +47,26 @@ def test_traffic_only_for_dispatched_kernels():
     assert t2 == tj["c2_gcc_phat"]["hbm_bytes_per_launch"] and "k_p1k_lean" in src
     # a kernel the committed passes were not taken on: no traffic figure
     real = bench.dominant_kernel
-    bench.dominant_kernel = lambda config, engine, first="": "k_not_profiled"
+    bench.dominant_kernel = lambda config, engine, first="", fused=True: "k_not_profiled"
     try:
         assert bench.traffic_entry(_args()) == (None, None)
     finally:
         bench.dominant_kernel = real
     for cfg in (3, 4):
-        t, src = bench.traffic_entry(_args("--config", str(cfg)))
         ks = tj[f"c{cfg}_gcc_phat"]["kernels"]
-        want = sum(v["hbm_bytes"] for k, v in ks.items() if k.split("<")[0] in ("k_frame16", "k_grid_bb"))
-        assert t == want and "k_frame16 + k_grid_bb" in src
+        with_grid = any(k.startswith("k_grid") for k in ks)
+        for fused in (False, True):
+            t, src = bench.traffic_entry(_args("--config", str(cfg)), "", fused)
+            if fused and with_grid:  # a pass with the separate grid kernel is not a fused launch's traffic
+                assert (t, src) == (None, None)
+            elif not fused and not with_grid:  # (and the reverse)
+                assert t is None
+            elif fused:
+                want = sum(v["hbm_bytes"] for k, v in ks.items() if k.split("<")[0] == "k_frame16")
+                assert t == want and "k_frame16" in src and "k_grid_bb" not in src
+            else:
+                want = sum(v["hbm_bytes"] for k, v in ks.items() if k.split("<")[0] in ("k_frame16", "k_grid_bb"))
+                assert t == want and "k_frame16 + k_grid_bb" in src
     t5, src5 = bench.stream_traffic(_args("--config", "5"))
     ks = tj["c5_direct"]["kernels"]
     assert t5 == sum(v["hbm_bytes"] for k, v in ks.items()

@@ -6,6 +6,13 @@ oracle (oracle/gcc_phat_oracle.py) with test_gpu_gcc_phat.py's tolerances:
   TDOA_F16_DEFER=0    k_frame16 with every pair's outputs in its round
   TDOA_F16_DEFER=1    k_frame16 with the deferred per-frame epilogue (at
                       C = 4096 the window table leaves no LDS for it: in-round)
+  TDOA_F16_FG=0 / 1   the grid by k_grid_bb after k_frame16 (compact weighted-
+                      score scratch) / solved inside k_frame16 by the last pair
+                      round's idle waves (the previous frame's scores kept in
+                      LDS); default: fused with the deferred epilogue (config
+                      4), k_grid_bb with in-round outputs (config 3)
+Every case also checks the cell / max_Lf bit for bit against the exhaustive
+float32 scan of the run's own weighted scores (vga_heatmap.h:99-108).
 
 The defaults (k_frame16, deferred at config 4, in-round at config 3) run in
 test_gpu_gcc_phat.py itself.
@@ -27,7 +34,7 @@ import numpy as np
 import gcc_phat_oracle as G
 from tdoa import synth
 from tdoa.localizer import Localizer
-from test_gpu_gcc_phat import check_phat, _np
+from test_gpu_gcc_phat import check_phat, _np, _grid_f32
 M, N = {M}, {N}
 xy = synth.square_mics(0.15) if M == 4 else synth.circle_mics(8, 0.15)
 kw = dict(num_mics=M, frame_len=N, sample_rate_hz=50000, mic_xy=xy)
@@ -40,6 +47,11 @@ fr = torch.cat([fr, fr2]).contiguous()
 got = _np(ph.localize(fr, scores=True))
 exp = G.gcc_phat_batch(fr.cpu().numpy(), S, ph.window(), ph.lut())
 check_phat(got, exp)
+cell, mx = _grid_f32(got["weighted_f"], ph.lut())
+assert (got["cell"] == cell).all() and (got["max_Lf"] == mx).all()
+lean = _np(ph.localize(fr))  # no scores requested: the bench's path
+for k in lean:
+    assert np.array_equal(lean[k], got[k]), k
 print("variant ok", ph.batch_kernel())
 """
 
@@ -48,6 +60,9 @@ print("variant ok", ph.batch_kernel())
     ({"TDOA_F16": "w"}, 8, 2048),
     ({"TDOA_F16_DEFER": "0"}, 8, 2048),
     ({"TDOA_F16_DEFER": "1"}, 4, 2048),  # one pair round, epilogue forced
+    ({"TDOA_F16_FG": "0"}, 8, 2048),  # config 4 with k_grid_bb after k_frame16
+    ({"TDOA_F16_FG": "1"}, 4, 4096),  # config 3 with the fused grid (in-round outputs)
+    ({"TDOA_F16_FG": "1", "TDOA_F16_DEFER": "0"}, 8, 2048),  # in-round outputs: double-buffered scores
 ])
 def test_frame16_variant_vs_fp64(env, M, N):
     code = CHILD.format(pkg=os.path.join(ROOT, "audio-triangulation_amd"), orc=os.path.join(ROOT, "oracle"),

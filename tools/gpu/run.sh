@@ -10,6 +10,7 @@
 #   kstats[:CFG[:ENGINE]] rocprofv3 --kernel-trace --stats of the bench
 #   pmc[:CFG[:ENGINE]]    FETCH_SIZE and WRITE_SIZE passes (one run each)
 #   sq[:CFG[:ENGINE]]     two SQ counter passes (waves, VALU, LDS, waits)
+#   flops[:CFG[:ENGINE]]  executed FP32 VALU flops (SQ_INSTS_VALU_FLOPS_FP32 + classes)
 #   pmcx:CFG:ENGINE:NAME:C1,C2,..  one pass of the listed counters (mind the
 #                         per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
 #   ablib[:L1,L2,..]      bench config 2 once per library tdoa/<L>.so (TDOA_LIB)
@@ -113,6 +114,15 @@ for step in "$@"; do
         prof "sq2_c${c}_$e" --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU \
             SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA || exit 27
         echo "sq c$c $e done"
+        ;;
+    flops)
+        # executed FP32 VALU work (SQ_INSTS_VALU_FLOPS_FP32 and the instruction
+        # classes) of a bench launch: flops[:CFG[:ENGINE]]
+        c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat)
+        PARGS="--config $c --engine $e --steps 24 --warmup 2 --no-cpu $BENCH_ARGS"
+        prof "flops_c${c}_$e" --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 \
+            SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU SQ_WAVES || exit 34
+        echo "flops c$c $e done"
         ;;
     pmcx)
         c=$(field "$step" 2 2); e=$(field "$step" 3 gcc_phat); n=$(field "$step" 4 x)

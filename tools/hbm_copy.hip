@@ -44,6 +44,24 @@ __global__ void __launch_bounds__(256) k_copy16(const v4u *__restrict__ src, v4u
         __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// the same copy with default-policy loads and stores (nt stores are not
+// write-through on gfx950, and the plain form is the guide's float4 copy)
+__global__ void __launch_bounds__(256) k_copy16p(const v4u *__restrict__ src, v4u *__restrict__ dst,
+                                                 size_t n16)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const v4u a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride)
+        dst[i] = src[i];
+}
+
 // read-only sweep (sum of words), the bound of a read-dominated kernel
 __global__ void __launch_bounds__(256) k_read16(const v4u *__restrict__ src, size_t n16, unsigned *sink)
 {
@@ -86,7 +104,8 @@ int main(int argc, char **argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    float ms_copy = 0.f, ms_read = 0.f;
+    float ms_copy = 0.f, ms_copyp = 0.f, ms_read = 0.f;
+    const dim3 gridp(cus * 4);  // plain copy: 4 x 256-thread workgroups per CU
     for (int pass = 0; pass < 2; pass++) {  // pass 0: warm-up (clocks, translations)
         CK(hipEventRecord(e0, 0));
         for (int i = 0; i < iters; i++)  // alternate directions: no buffer stays cached
@@ -96,19 +115,27 @@ int main(int argc, char **argv)
         CK(hipEventElapsedTime(&ms_copy, e0, e1));
         CK(hipEventRecord(e0, 0));
         for (int i = 0; i < iters; i++)
+            hipLaunchKernelGGL(k_copy16p, gridp, block, 0, 0, (i & 1) ? b : a, (i & 1) ? a : b, n16);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms_copyp, e0, e1));
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; i++)
             hipLaunchKernelGGL(k_read16, grid, block, 0, 0, (i & 1) ? b : a, n16, sink);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms_read, e0, e1));
     }
     CK(hipGetLastError());
-    const double t_copy = ms_copy / 1e3 / iters, t_read = ms_read / 1e3 / iters;
+    const double t_copy = ms_copy / 1e3 / iters, t_read = ms_read / 1e3 / iters, t_copyp = ms_copyp / 1e3 / iters;
     printf("{\"kernel\": \"k_copy16\", \"mib_per_buffer\": %zu, \"iterations\": %d, \"grid\": %u, "
            "\"copy_bytes_per_launch\": %zu, \"copy_us\": %.3f, \"copy_gbs\": %.1f, "
+           "\"copy_plain_kernel\": \"k_copy16p\", \"copy_plain_grid\": %u, \"copy_plain_us\": %.3f, "
+           "\"copy_plain_gbs\": %.1f, "
            "\"read_kernel\": \"k_read16\", \"read_bytes_per_launch\": %zu, \"read_us\": %.3f, "
            "\"read_gbs\": %.1f}\n",
-           mib, iters, grid.x, 2 * bytes, t_copy * 1e6, 2.0 * bytes / t_copy / 1e9, bytes, t_read * 1e6,
-           (double)bytes / t_read / 1e9);
+           mib, iters, grid.x, 2 * bytes, t_copy * 1e6, 2.0 * bytes / t_copy / 1e9, gridp.x, t_copyp * 1e6,
+           2.0 * bytes / t_copyp / 1e9, bytes, t_read * 1e6, (double)bytes / t_read / 1e9);
     CK(hipFree(a));
     CK(hipFree(b));
     CK(hipFree(sink));
