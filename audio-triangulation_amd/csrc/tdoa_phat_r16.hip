@@ -1078,7 +1078,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     if constexpr (FG) {
         const int fo = (int)(((char *)(scl + (DM == 1 ? P * kp.K : 0)) - smem + 15) & ~15);
         fgl.w = (float *)(smem + fo);
-        fgl.bnd = fgl.w + 2 * CKp;
+        fgl.bnd = fgl.w + (DM == 0 ? 2 : 1) * CKp;  // DM 1: one buffer (written after the last round)
         fgl.key = (uint64_t *)(fgl.bnd + 256);
         fgl.cand = (int *)(fgl.key + 2 * FG_NGW);
     }
@@ -1537,10 +1537,12 @@ constexpr bool fg_shape()
     constexpr int G = 16384 / C, P = M * (M - 1) / 2, ROUNDS = (P + G - 1) / G, GI0 = P - (ROUNDS - 1) * G;
     return (G - GI0) * (C / 16 / 64) >= FG_NGW;
 }
-// TDOA_F16_FG: 1 on, 0 off, skip (A/B of the bare FG structure); unset: on
-// with the deferred epilogue only (config 4: time-neutral, 92.98 vs 93.04 ms per
-// step, and no weighted-score round trip through HBM), off with in-round
-// outputs (config 3: 4.04 vs 3.50 ms -- its k_grid_bb is cheap)
+// TDOA_F16_FG: 1 on, skip (A/B of the bare FG structure); unset or 0: off.
+// Measured slower at both shapes it applies to (same box, ms per step):
+// config 3 4.04 vs 3.50, config 4 100.9 vs 93.0 (k_frame16 + k_grid_bb) -- the
+// last round's idle waves hold one frame's dependent search chain (bounds, then
+// entry evaluations on L2 tuple rows) and it outlasts the round; k_grid_bb
+// hides the same chains behind other frames' (DESIGN.md "Fused grid")
 static int fg_mode()
 {
     static const int m = [] {
@@ -1551,10 +1553,12 @@ static int fg_mode()
     }();
     return m;
 }
-static size_t fg_lds_bytes(const tdoa_kparams &kp)
+static size_t fg_lds_bytes(const tdoa_kparams &kp, bool defer)
 {
+    // DM 0 double-buffers the compact scores by iteration; DM 1 writes them in
+    // the epilogue, after the last round that reads the previous frame's
     const size_t CKp = (size_t)((kp.wc_CK + 3) & ~3);
-    return 16 + 2 * CKp * 4 + 256 * 4 + 2 * FG_NGW * 8 + FG_NGW * 4;
+    return 16 + (defer ? 1 : 2) * CKp * 4 + 256 * 4 + 2 * FG_NGW * 8 + FG_NGW * 4;
 }
 template <int C, int M>
 static bool frame16_defer(const tdoa_kparams &kp)
@@ -1577,10 +1581,10 @@ static bool frame16_fg(const tdoa_kparams &kp)
     if (!fg_shape<C, M>() || !kp.fg_ok || !kp.fg_q || !kp.fg_tup || fg_mode() == 0 || kp.P != M * (M - 1) / 2)
         return false;
     const bool defer = frame16_defer<C, M>(kp);
-    if (fg_mode() < 0 && !defer)
+    if (fg_mode() < 0)
         return false;
     const size_t base = frame16_lds_base<C>() + (defer ? (size_t)kp.P * kp.K * sizeof(float) : 0);
-    return base + fg_lds_bytes(kp) <= 160 * 1024;
+    return base + fg_lds_bytes(kp, defer) <= 160 * 1024;
 }
 
 template <int C, int M>
@@ -1601,7 +1605,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
         fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
     const size_t lds =
         (defer ? frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float) : frame16_lds_base<C>()) +
-        (fg ? fg_lds_bytes(kp) : 0);
+        (fg ? fg_lds_bytes(kp, defer) : 0);
     tdoa_kparams kpl = kp;
     if (fg && fg_mode() == 2)
         kpl.fg_ok = 2;  // A/B only: the FG kernel without its grid work (no grid outputs)

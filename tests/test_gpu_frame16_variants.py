@@ -6,11 +6,11 @@ oracle (oracle/gcc_phat_oracle.py) with test_gpu_gcc_phat.py's tolerances:
   TDOA_F16_DEFER=0    k_frame16 with every pair's outputs in its round
   TDOA_F16_DEFER=1    k_frame16 with the deferred per-frame epilogue (at
                       C = 4096 the window table leaves no LDS for it: in-round)
-  TDOA_F16_FG=0 / 1   the grid by k_grid_bb after k_frame16 (compact weighted-
-                      score scratch) / solved inside k_frame16 by the last pair
-                      round's idle waves (the previous frame's scores kept in
-                      LDS); default: fused with the deferred epilogue (config
-                      4), k_grid_bb with in-round outputs (config 3)
+  TDOA_F16_FG=1       the grid solved inside k_frame16 by the last pair round's
+                      idle waves (the previous frame's compact scores kept in
+                      LDS: one buffer with the deferred epilogue, two with
+                      in-round outputs) instead of by k_grid_bb after it (the
+                      default: measured faster at both shapes)
 Every case also checks the cell / max_Lf bit for bit against the exhaustive
 float32 scan of the run's own weighted scores (vga_heatmap.h:99-108).
 
@@ -60,7 +60,7 @@ print("variant ok", ph.batch_kernel())
     ({"TDOA_F16": "w"}, 8, 2048),
     ({"TDOA_F16_DEFER": "0"}, 8, 2048),
     ({"TDOA_F16_DEFER": "1"}, 4, 2048),  # one pair round, epilogue forced
-    ({"TDOA_F16_FG": "0"}, 8, 2048),  # config 4 with k_grid_bb after k_frame16
+    ({"TDOA_F16_FG": "1"}, 8, 2048),  # config 4, deferred epilogue: one score buffer
     ({"TDOA_F16_FG": "1"}, 4, 4096),  # config 3 with the fused grid (in-round outputs)
     ({"TDOA_F16_FG": "1", "TDOA_F16_DEFER": "0"}, 8, 2048),  # in-round outputs: double-buffered scores
 ])

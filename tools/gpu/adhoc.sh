@@ -1,10 +1,6 @@
 set -o pipefail
-export TAG=m2
-tools/gpu/run.sh test:tests/test_gpu_frame16_variants.py,tests/test_gpu_bench_path.py && \
-STEPS=5 ROUNDS=1 BENCH_ARGS="--config 4 --no-parity" tools/gpu/run.sh abenv:TDOA_F16_FG:1,0,skip && \
-STEPS=20 ROUNDS=1 BENCH_ARGS="--config 3 --no-parity" tools/gpu/run.sh abenv:TDOA_F16_FG:1,0,skip && \
-STEPS=50 tools/gpu/run.sh kstats:5 && \
-tools/gpu/run.sh flops:2 && \
-BENCH_ARGS="--batch 65536" tools/gpu/run.sh flops:3 && \
-BENCH_ARGS="--batch 131072" tools/gpu/run.sh flops:4 && \
-tools/gpu/run.sh calib
+export TAG=d5
+mkdir -p gpurun_out/$TAG
+tools/gpu/run.sh diagf16:4 && \
+timeout -k 10 120 python tools/diag_grid_bb.py 4 262144 > gpurun_out/$TAG/diag_bb_c4.txt 2>&1 && cat gpurun_out/$TAG/diag_bb_c4.txt && \
+tools/gpu/run.sh test:tests/test_gpu_frame16_variants.py

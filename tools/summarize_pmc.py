@@ -45,7 +45,10 @@ def main():
         wr = 1024.0 * (sum(w.get(k, [0])) / max(1, len(w.get(k, []))))
         kernels[k] = {"hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes": rd + wr,
                       "dispatches": len(f.get(k, []))}
-    total = sum(v["hbm_bytes"] for k, v in kernels.items() if v["dispatches"])
+    # the launch's kernels: dispatched once per bench step (a kernel dispatched far
+    # fewer times -- the parity report's DIRECT run -- is not part of the launch)
+    top = max((v["dispatches"] for v in kernels.values()), default=0)
+    total = sum(v["hbm_bytes"] for k, v in kernels.items() if v["dispatches"] and v["dispatches"] * 2 >= top)
     dk = next((v for k, v in kernels.items() if dom in k), None)
     out = json.load(open(dst)) if os.path.exists(dst) else {}
     out["note"] = ("per launch; read = 2 x FETCH_SIZE KiB (gfx950 wide-load correction), write = "
