@@ -115,6 +115,11 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 // below is a per-thread base and a compile-time part (an offset, or one XOR)
 // -- see ColIdx and the pass writes.  The padding's C / 16 elements per buffer
 // are freed (8 KiB at config 4).
+// the DM 1 epilogue four pairs per wave (frame16_out16); F16_OUT16=0: a wave
+// per pair, two interleaved (frame16_pair_out<2>)
+#ifndef F16_OUT16
+#define F16_OUT16 1
+#endif
 #ifndef F16_XS
 #define F16_XS 1
 #endif
@@ -561,7 +566,7 @@ __device__ __forceinline__ void static_for(F &&f)
 __device__ unsigned long long g_diag_f16[1 << 16];
 #define F16_MARK()                                       \
     do {                                                 \
-        if (nst < 29)                                    \
+        if (nst < NSTAMP - 3)                            \
             stamp[nst++] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
@@ -828,6 +833,61 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
             out.lags[fr * P + p[h]] = b - S;
             lagl[p[h]] = b - S;
         }
+    }
+}
+
+// The DM 1 epilogue's outputs, four pairs per wave: 16-lane row q of the wave
+// takes pair p, lane r of the row its lags r + 16 i (i < KL; K <= 16 KL).  The
+// first maximum is a row reduction (four DPP steps, no cross-row moves) and
+// every row instruction serves four pairs, where frame16_pair_out spends a
+// whole wave (and a wave reduction) on one -- its VALU work, 8 % of a config-4
+// frame, was the epilogue's cost.  Same values, same tie rule (ascending lags
+// per lane with a strict '>', then the smallest lag among equal keys), same
+// stores.  wlo, ww, woff: this lane's pair's compact-scratch range.
+template <int KL>
+__device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa_kout &out, const float *scl,
+                                              const float *priorl, int *lagl, int64_t fr, int P, int p, int r,
+                                              int wlo, int ww, int woff)
+{
+    const int K = kp.K, S = kp.S;
+    float sv[KL];
+    int bkey = INT_MIN, bk = INT_MAX;
+#pragma unroll
+    for (int i = 0; i < KL; i++) {
+        const int k = r + 16 * i;
+        sv[i] = k < K ? scl[p * K + k] : 0.0f;
+        const int key = fkey(sv[i]);
+        if (k < K && key > bkey) {
+            bkey = key;
+            bk = k;
+        }
+    }
+    const int mk = row_reduce<true>(bkey);
+    bk = row_reduce<false>(bkey == mk ? bk : INT_MAX);
+    const int b = bk < 0 ? 0 : (bk >= K ? K - 1 : bk);  // NaN scores: keep the index in range
+    const size_t gb = (size_t)(fr * P + p) * K;
+    float *wc = kernarg_out()->weighted_c;
+    float *pk3 = kernarg_out()->peak3;
+    float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + woff - wlo : nullptr;
+#pragma unroll
+    for (int i = 0; i < KL; i++) {
+        const int k = r + 16 * i;
+        if (k < K) {
+            const int dd = k > b ? k - b : b - k;
+            const float wv = sv[i] * priorl[dd];
+            if (out.scores_f)
+                out.scores_f[gb + k] = sv[i];
+            if (out.weighted_f)
+                out.weighted_f[gb + k] = wv;
+            if (wcp && k >= wlo && k < wlo + ww)
+                wcp[k] = wv;
+            if (pk3 && k >= b - 1 && k <= b + 1)
+                pk3[(size_t)(fr * P + p) * 3 + 1 - b + k] = sv[i];
+        }
+    }
+    if (r == 0) {
+        out.lags[fr * P + p] = b - S;
+        lagl[p] = b - S;
     }
 }
 
@@ -1141,9 +1201,24 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         rl_w[r] = __builtin_amdgcn_readfirstlane(kp.wc_w[q]);
         rl_off[r] = __builtin_amdgcn_readfirstlane(kp.wc_off[q]);
     }
+    // DM 1 (frame16_out16): this lane's pair 4 w + (lane >> 4) and its compact range
+    constexpr bool OUT16 = DM == 1 && !FG && F16_OUT16 != 0;
+    int e16_p = 0, e16_lo = 0, e16_w = 0, e16_off = 0;
+    if constexpr (OUT16) {
+        e16_p = (int)threadIdx.x >> 4;  // wave w, row q: pair 4 w + q
+        const int pq = e16_p < P ? e16_p : 0;
+        // per-lane loads, waited for below (selecting each row's range from four
+        // scalar loads gave wrong compact offsets for some pairs with this
+        // compiler: bench-path test cfg4, cells 72 % equal; not understood)
+        const auto *kk = kernarg_kp();
+        e16_lo = kk->wc_lo[pq];
+        e16_w = kk->wc_w[pq];
+        e16_off = kk->wc_off[pq];
+        asm volatile("" : "+v"(e16_lo), "+v"(e16_w), "+v"(e16_off));
+    }
     // DM 1: the epilogue's pairs w, w + 16
     int ep_lo[2] = {0, 0}, ep_w[2] = {0, 0}, ep_off[2] = {0, 0};
-    if constexpr (DM == 1) {
+    if constexpr (DM == 1 && !OUT16) {
         const int w0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -1154,7 +1229,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
     }
 #ifdef TDOA_DIAG
-    unsigned long long stamp[32] = {};
+    constexpr int NSTAMP = 48;  // k_frame16: up to 45 phase marks (config 4: 33)
+    unsigned long long stamp[NSTAMP] = {};
     int nst = 0;
     const int64_t diag_fr = blockIdx.x + (B >= (int64_t)(F16_DIAG_FRAME + 1) * gridDim.x ? F16_DIAG_FRAME : 0) *
                                              (int64_t)gridDim.x;
@@ -1209,7 +1285,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     const bool fgr = FG && prev >= 0 && kp.fg_ok == 1;  // (fg_ok 2: TDOA_F16_FG=skip, A/B of the bare structure)
     if (fr == diag_fr) {
 #ifdef TDOA_DIAG
-        stamp[30] = __builtin_amdgcn_s_memrealtime();
+        stamp[NSTAMP - 2] = __builtin_amdgcn_s_memrealtime();
 #endif
         F16_MARK();
     }
@@ -1454,6 +1530,16 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // lags l and l + 64, K <= 127)
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
         static_assert(P <= 32, "two epilogue pairs per wave at most");
+        if constexpr (OUT16) {
+            // waves 0 .. ceil(P / 4) - 1, four pairs each (rows past P idle)
+            pin_words();
+            if (4 * wv < P && e16_p < P) {
+                if (K <= 96)
+                    frame16_out16<6>(kp, out, scl, priorl, lagl, fr, P, e16_p, ln & 15, e16_lo, e16_w, e16_off);
+                else
+                    frame16_out16<8>(kp, out, scl, priorl, lagl, fr, P, e16_p, ln & 15, e16_lo, e16_w, e16_off);
+            }
+        } else {
         const bool oka = ln < K, okb = ln + 64 < K;
         const int pp[2] = {wv, wv + 16 < P ? wv + 16 : wv};
         const bool on2[2] = {wv < P, wv + 16 < P};
@@ -1467,6 +1553,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on2[0])
             frame16_pair_out<2>(kp, out, priorl, lagl, fr, P, pp, on2, ln, ln + 64, oka, okb, sa, sb, ln == 0, ep_lo,
                                 ep_w, ep_off, fgw);
+        }
         __syncthreads();  // lagl complete for the gate; scl free for the next frame
         if (fr == diag_fr)
             F16_MARK();
@@ -1482,8 +1569,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     fpar ^= 1;
 #ifdef TDOA_DIAG
     if (fr == diag_fr) {
-        stamp[31] = __builtin_amdgcn_s_memrealtime();
-        stamp[29] = __builtin_amdgcn_s_memtime();
+        stamp[NSTAMP - 1] = __builtin_amdgcn_s_memrealtime();
+        stamp[NSTAMP - 3] = __builtin_amdgcn_s_memtime();
     }
 #endif
     }  // frames
@@ -1521,9 +1608,9 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
     }
 #ifdef TDOA_DIAG
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 128)
-        for (int i = 0; i < 32; i++)
-            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + i] = stamp[i];
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 64)
+        for (int i = 0; i < NSTAMP; i++)
+            g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * NSTAMP + i] = stamp[i];
 #endif
 }
 #undef F16_MARK
@@ -1786,7 +1873,7 @@ __device__ __forceinline__ f2 frame16w_inverse(const f2 *Ui, const f2 *Uj, const
 #ifdef TDOA_DIAG
 #define F16W_MARK()                                      \
     do {                                                 \
-        if (nst < 29)                                    \
+        if (nst < NSTAMP - 3)                            \
             stamp[nst++] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
@@ -1843,7 +1930,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16w(tdoa_kparams kp, tdoa_kout
     const f2 oml = tw[32 * lane];   // W_64^l = W_C^{32 l}
     const f2 *tt = ttl;  // visible after the first barrier (the DC sum's)
 #ifdef TDOA_DIAG
-    unsigned long long stamp[32] = {};
+    constexpr int NSTAMP = 32;
+    unsigned long long stamp[NSTAMP] = {};
     int nst = 0;
     const int64_t diag_fr = blockIdx.x + (B >= (int64_t)(F16_DIAG_FRAME + 1) * gridDim.x ? F16_DIAG_FRAME : 0) *
                                              (int64_t)gridDim.x;

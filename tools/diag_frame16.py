@@ -31,12 +31,13 @@ L = tdoa.load()
 L.tdoa_diag_fetch_f16.argtypes = [C.c_void_p, C.c_int]
 buf = np.zeros(1 << 16, np.uint64)
 assert L.tdoa_diag_fetch_f16(buf.ctypes.data_as(C.c_void_p), 1 << 16) == 0
-st = buf.reshape(-1, 32).astype(np.int64)
+wave_kernel = cfg == 4 and os.environ.get("TDOA_F16", "grp") == "w"  # k_frame16w
+W = 32 if wave_kernel else 48  # stamps per wave record; the last three: end memtime, start / end realtime
+st = buf[:(len(buf) // W) * W].reshape(-1, W).astype(np.int64)
 st = st[st[:, 0] > 0]
 G = 16384 // N
 P = M * (M - 1) // 2
 R = (P + G - 1) // G
-wave_kernel = cfg == 4 and os.environ.get("TDOA_F16", "grp") == "w"  # k_frame16w
 if wave_kernel:
     # k_frame16w: start, forward, split, then one stamp per pair of the wave
     # (waves 0-11 run two pairs, 12-15 one: their stamp 4 stays 0)
@@ -63,12 +64,12 @@ else:
         names.append("epilogue")  # the deferred pair outputs (DM 1)
 n = len(names)
 print(f"config {cfg}: M={M} N={N} P={P} G={G} rounds={R}, waves {len(st)}")
-life = st[:, 29] - st[:, 0]
+life = st[:, W - 3] - st[:, 0]
 print("wave life (cycles): p50 %.0f; clock %.2f GHz" % (np.median(life),
-      np.median(life / ((st[:, 31] - st[:, 30]) / 100e6)) / 1e9))
+      np.median(life / ((st[:, W - 1] - st[:, W - 2]) / 100e6)) / 1e9))
 print("phase durations (cycles): p10 / p50 / p90")
 for i in range(1, n):
     d = st[:, i] - st[:, i - 1]
     print(f"  {names[i]:9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
-d = st[:, 29] - st[:, n - 1] if not wave_kernel else st[:, 29] - np.where(st[:, 4] > 0, st[:, 4], st[:, 3])
+d = st[:, W - 3] - st[:, n - 1] if not wave_kernel else st[:, W - 3] - np.where(st[:, 4] > 0, st[:, 4], st[:, 3])
 print(f"  {'tail':9s} {np.percentile(d, 10):8.0f} {np.median(d):8.0f} {np.percentile(d, 90):8.0f}")
