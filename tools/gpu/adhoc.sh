@@ -1,4 +1,5 @@
 set -o pipefail
-export TAG=c3d
+export TAG=sub
 mkdir -p gpurun_out/$TAG
-STEPS=20 ROUNDS=2 BENCH_ARGS="--config 3" tools/gpu/run.sh abenv:TDOA_F16_DEFER:0,1
+tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_parity.py,tests/test_gpu_bench_path.py && \
+STEPS=400 tools/gpu/run.sh ablib:libtdoa,libtdoa_subor,libtdoa,libtdoa_subor,libtdoa,libtdoa_subor
