@@ -120,6 +120,11 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_OUT16
 #define F16_OUT16 1
 #endif
+// timing only (A/B builds): no per-pair outputs at all (lags, compact scores, grid
+// inputs wrong) -- what the output stage costs
+#ifndef F16_NO_OUT
+#define F16_NO_OUT 0
+#endif
 #ifndef F16_XS
 #define F16_XS 1
 #endif
@@ -1506,6 +1511,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 const int pp[1] = {p}, lo[1] = {rl_lo[RI]}, wd[1] = {rl_w[RI]}, of[1] = {rl_off[RI]};
                 const bool on1[1] = {true};
                 const float a1[1] = {sa}, b1[1] = {sb};
+                if (!F16_NO_OUT)
                 frame16_pair_out<1>(kp, out, priorl, lagl, fr, P, pp, on1, ka, kb, oka, okb, a1, b1, l == 0, lo, wd,
                                     of, fgw);
             }
@@ -1533,7 +1539,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if constexpr (OUT16) {
             // waves 0 .. ceil(P / 4) - 1, four pairs each (rows past P idle)
             pin_words();
-            if (4 * wv < P && e16_p < P) {
+            if (!F16_NO_OUT && 4 * wv < P && e16_p < P) {
                 if (K <= 96)
                     frame16_out16<6>(kp, out, scl, priorl, lagl, fr, P, e16_p, ln & 15, e16_lo, e16_w, e16_off);
                 else

@@ -16,6 +16,14 @@
  *   gcc -std=gnu11 -Ihost/pico_host -I<reference>/src -I../include \
  *       host/sample_compute_main.c -Ltdoa -ltdoa -lamdhip64 -lm
  * Run: ./sample_compute_host [frames]   (needs a gfx950 GPU)
+ *
+ * Environment:
+ *   TDOA_REF_HOST=1    libtdoa's host path for the per-frame symbols
+ *                      (tdoa_ref_set_device(-1): no HIP call, runs without a GPU)
+ *   TDOA_REF_LOG=path  at every hand-off, the loop's state as the reference's own
+ *                      structs (int64 sample, u64 now_us, then mic_a/b/c_rb,
+ *                      buffer_a/b/c, new_corr_ab/ac/bc, corr_ab/ac/bc) for
+ *                      tests/test_reference_loop.py to check against the oracle
  */
 #include <math.h>
 #include <stdint.h>
@@ -26,6 +34,9 @@
 
 /* libtdoa's clock hook (tdoa_reference_abi.h): the EMA's get_absolute_time() */
 void tdoa_ref_set_clock(absolute_time_t (*now_us)(void));
+int tdoa_ref_set_device(int device);
+
+static FILE *g_log;
 
 volatile uint8_t dma_sample_array[3];
 
@@ -90,6 +101,25 @@ static PT_THREAD(protothread_host_consumer(struct pt *pt))
     while (true) {
         PT_SEM_WAIT(pt, &vga_semaphore);
         g_frames++;
+        if (g_log) {
+            const int64_t smp = g_sample;
+            const uint64_t now = (uint64_t)g_now;
+            fwrite(&smp, sizeof smp, 1, g_log);
+            fwrite(&now, sizeof now, 1, g_log);
+            fwrite(&mic_a_rb, sizeof mic_a_rb, 1, g_log);
+            fwrite(&mic_b_rb, sizeof mic_b_rb, 1, g_log);
+            fwrite(&mic_c_rb, sizeof mic_c_rb, 1, g_log);
+            fwrite(&buffer_a, sizeof buffer_a, 1, g_log);
+            fwrite(&buffer_b, sizeof buffer_b, 1, g_log);
+            fwrite(&buffer_c, sizeof buffer_c, 1, g_log);
+            fwrite(&new_corr_ab, sizeof new_corr_ab, 1, g_log);
+            fwrite(&new_corr_ac, sizeof new_corr_ac, 1, g_log);
+            fwrite(&new_corr_bc, sizeof new_corr_bc, 1, g_log);
+            fwrite(&corr_ab, sizeof corr_ab, 1, g_log);
+            fwrite(&corr_ac, sizeof corr_ac, 1, g_log);
+            fwrite(&corr_bc, sizeof corr_bc, 1, g_log);
+            fflush(g_log);
+        }
         printf("frame %d at sample %ld: best shifts ab %d ac %d bc %d (EMA ab %d ac %d bc %d)\n",
                g_frames, g_sample, new_corr_ab.best_shift, new_corr_ac.best_shift,
                new_corr_bc.best_shift, corr_ab.best_shift, corr_ac.best_shift, corr_bc.best_shift);
@@ -107,6 +137,12 @@ int main(int argc, char **argv)
 {
     if (argc > 1)
         g_want = atoi(argv[1]);
+    const char *host = getenv("TDOA_REF_HOST");
+    if (host && atoi(host) == 1 && tdoa_ref_set_device(-1) != 0)
+        return 3;
+    const char *log = getenv("TDOA_REF_LOG");
+    if (log && !(g_log = fopen(log, "wb")))
+        return 4;
     tdoa_ref_set_clock(host_now_us);
     capture_next();
     PT_SEM_INIT(&vga_semaphore, 0);

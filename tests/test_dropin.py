@@ -3,8 +3,9 @@ loop -- src/sample_compute.h, unchanged, with the reference's component
 headers -- compiles against include/'s ABI and links against libtdoa.so
 alone for every component symbol (rolling_buffer_*, buffer_*, correlations_*),
 with host/pico_host/ replacing the Pico SDK side (capture, clock, protothread
-primitives).  Link-only (it runs on a GPU; the GPU box has no /root/reference,
-and nothing built here is shipped): skipped where the reference is absent.
+primitives).  Link check; tests/test_reference_loop.py RUNS the same program on
+libtdoa's host path and checks every hand-off against the oracle.  Skipped where
+the reference is absent (the GPU box); nothing built here is shipped.
 The reference's component .c files are NOT compiled: libtdoa provides them."""
 import os
 import shutil

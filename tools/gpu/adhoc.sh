@@ -1,5 +1,5 @@
 set -o pipefail
-export TAG=sub
+export TAG=noout
 mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_parity.py,tests/test_gpu_bench_path.py && \
-STEPS=400 tools/gpu/run.sh ablib:libtdoa,libtdoa_subor,libtdoa,libtdoa_subor,libtdoa,libtdoa_subor
+STEPS=5 BENCH_ARGS="--config 4 --no-parity --no-cpu" tools/gpu/run.sh ablib:libtdoa,libtdoa_noout,libtdoa,libtdoa_noout && \
+STEPS=20 BENCH_ARGS="--config 3 --no-parity --no-cpu" tools/gpu/run.sh ablib:libtdoa,libtdoa_noout,libtdoa,libtdoa_noout
