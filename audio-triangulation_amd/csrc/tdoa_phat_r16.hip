@@ -120,6 +120,12 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_OUT16
 #define F16_OUT16 1
 #endif
+// DM 1 with the four-pairs epilogue: the epilogue of frame f runs in frame
+// f + 1's forward, after its pass-3 stores (F16_EPI_LAG=0: after frame f's
+// last round, the workgroup waiting)
+#ifndef F16_EPI_LAG
+#define F16_EPI_LAG 1
+#endif
 // timing only (A/B builds): no per-pair outputs at all (lags, compact scores, grid
 // inputs wrong) -- what the output stage costs
 #ifndef F16_NO_OUT
@@ -586,10 +592,16 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 // ends in buf at pidx(j + T q), after a closing barrier
 // WM: where the thread's window words come from -- 0 global (L2), 1 LDS (win
 // is the LDS copy), 2 registers (wr, loaded once per launch)
-template <int C, int WM, typename Mark, bool XS = false>
+struct NoHook16 {
+    __device__ void operator()() const {}
+};
+// hook: called once every thread's pass-3 stores are issued, before the
+// closing barrier (an LDS-store-bound interval whose VALU is idle):
+// k_frame16's lagged epilogue runs the previous frame's outputs there
+template <int C, int WM, typename Mark, bool XS = false, typename Hook = NoHook16>
 __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, const uint32_t (&wr)[8],
                                                 f2 *buf, int *red, const f2 *tt, int tid, int g, int j, int pj,
-                                                int log2N, Mark mark)
+                                                int log2N, Mark mark, Hook hook = Hook())
 {
     constexpr int T = C / 16, R1 = C / 256;
     const ColIdx<C, XS> cj(j);  // XS: pj is unused (the column reads / writes go through cj)
@@ -713,6 +725,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
             buf[XS ? cj.at(q) : pj + po(T * q)] = v[brev<16>(q)];
     }
+    hook();
     __syncthreads();
     mark();
 }
@@ -1208,19 +1221,42 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
     // DM 1 (frame16_out16): this lane's pair 4 w + (lane >> 4) and its compact range
     constexpr bool OUT16 = DM == 1 && !FG && F16_OUT16 != 0;
-    int e16_p = 0, e16_lo = 0, e16_w = 0, e16_off = 0;
+    // (one register: lo | w << 8 | off << 16; the lagged epilogue runs where the
+    // forward's registers peak)
+    uint32_t e16_rng = 0;
     if constexpr (OUT16) {
-        e16_p = (int)threadIdx.x >> 4;  // wave w, row q: pair 4 w + q
+        const int e16_p = (int)threadIdx.x >> 4;  // wave w, row q: pair 4 w + q
         const int pq = e16_p < P ? e16_p : 0;
         // per-lane loads, waited for below (selecting each row's range from four
         // scalar loads gave wrong compact offsets for some pairs with this
         // compiler: bench-path test cfg4, cells 72 % equal; not understood)
         const auto *kk = kernarg_kp();
-        e16_lo = kk->wc_lo[pq];
-        e16_w = kk->wc_w[pq];
-        e16_off = kk->wc_off[pq];
-        asm volatile("" : "+v"(e16_lo), "+v"(e16_w), "+v"(e16_off));
+        e16_rng = (uint32_t)kk->wc_lo[pq] | (uint32_t)kk->wc_w[pq] << 8 | (uint32_t)kk->wc_off[pq] << 16;
+        asm volatile("" : "+v"(e16_rng));
     }
+    // DM 1 (four-pairs epilogue), lagged (F16_EPI_LAG): frame f's outputs run in
+    // frame f + 1's forward, after its pass-3 stores; its gate after that forward
+    constexpr bool ELAG = OUT16 && F16_EPI_LAG != 0;
+    auto epi16 = [&](int64_t f) {
+        const int t = opaque_idx((int)threadIdx.x);
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = t >> 4;
+        if (!F16_NO_OUT && 4 * wv < P && pe < P) {
+            const int r = t & 15, lo = (int)(e16_rng & 0xFFu), wd = (int)((e16_rng >> 8) & 0xFFu),
+                      of = (int)(e16_rng >> 16);
+            if (kp.K <= 96)
+                frame16_out16<6>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
+            else
+                frame16_out16<8>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
+        }
+    };
+    auto gate_of = [&](int64_t f) {
+        if (threadIdx.x == 0 && out.gate) {
+            int tot = 0;
+            for (int q = 0; q < P; q++)
+                tot += lagl[q] * lagl[q];
+            out.gate[f] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+        }
+    };
     // DM 1: the epilogue's pairs w, w + 16
     int ep_lo[2] = {0, 0}, ep_w[2] = {0, 0}, ep_off[2] = {0, 0};
     if constexpr (DM == 1 && !OUT16) {
@@ -1300,8 +1336,19 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (fr == diag_fr)
             F16_MARK();  // the forward's barriers (diagnostic build)
     };
-    frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS>(w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt,
-                                                                    tid, g, j, pj, kp.log2N, fwd_mark);
+    if constexpr (ELAG) {
+        auto lag_hook = [&] {
+            if (prev >= 0)
+                epi16(prev);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
+        };
+        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS, decltype(lag_hook)>(
+            w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N, fwd_mark, lag_hook);
+        if (prev >= 0)
+            gate_of(prev);  // its lags are in lagl since the forward's closing barrier
+    } else {
+        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS>(w, f16_win_lds<C>() ? winl : win, wr, buf, red,
+                                                                        tt, tid, g, j, pj, kp.log2N, fwd_mark);
+    }
     if (fr == diag_fr)
         F16_MARK();  // forward transforms done
     // split + unit normalisation of every mic at this thread's bin pairs:
@@ -1537,13 +1584,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
         static_assert(P <= 32, "two epilogue pairs per wave at most");
         if constexpr (OUT16) {
-            // waves 0 .. ceil(P / 4) - 1, four pairs each (rows past P idle)
-            pin_words();
-            if (!F16_NO_OUT && 4 * wv < P && e16_p < P) {
-                if (K <= 96)
-                    frame16_out16<6>(kp, out, scl, priorl, lagl, fr, P, e16_p, ln & 15, e16_lo, e16_w, e16_off);
-                else
-                    frame16_out16<8>(kp, out, scl, priorl, lagl, fr, P, e16_p, ln & 15, e16_lo, e16_w, e16_off);
+            // waves 0 .. ceil(P / 4) - 1, four pairs each (rows past P idle);
+            // ELAG: in the next frame's forward (or after the loop) instead
+            if constexpr (!ELAG) {
+                pin_words();
+                epi16(fr);
             }
         } else {
         const bool oka = ln < K, okb = ln + 64 < K;
@@ -1560,17 +1605,15 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             frame16_pair_out<2>(kp, out, priorl, lagl, fr, P, pp, on2, ln, ln + 64, oka, okb, sa, sb, ln == 0, ep_lo,
                                 ep_w, ep_off, fgw);
         }
-        __syncthreads();  // lagl complete for the gate; scl free for the next frame
-        if (fr == diag_fr)
-            F16_MARK();
+        if constexpr (!ELAG) {
+            __syncthreads();  // lagl complete for the gate; scl free for the next frame
+            if (fr == diag_fr)
+                F16_MARK();
+        }
     }
     pin_words();
-    if (tid == 0 && out.gate) {
-        int tot = 0;
-        for (int q = 0; q < P; q++)
-            tot += lagl[q] * lagl[q];
-        out.gate[fr] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
-    }
+    if constexpr (!ELAG)
+        gate_of(fr);
     prev = fr;
     fpar ^= 1;
 #ifdef TDOA_DIAG
@@ -1580,6 +1623,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 #endif
     }  // frames
+    if constexpr (ELAG) {
+        // the last frame's outputs (its last round closed with a barrier: scl complete)
+        if (prev >= 0) {
+            epi16(prev);
+            __syncthreads();
+            gate_of(prev);
+        }
+    }
     if constexpr (FG) {
         // the last frame's grid, by waves 0 .. FG_NGW - 1 (every buffer is free)
         if (prev >= 0 && kp.fg_ok == 1) {
