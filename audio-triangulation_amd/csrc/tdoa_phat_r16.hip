@@ -1707,9 +1707,10 @@ static size_t fg_lds_bytes(const tdoa_kparams &kp, bool defer)
 template <int C, int M>
 static bool frame16_defer(const tdoa_kparams &kp)
 {
-    // deferred pair outputs (DM 1) at three or more pair rounds when the
-    // frame's [P][K] scores fit next to the buffers (config 4: 10.4 KiB of 13.3
-    // free; 98.5 vs 104.4 ms per step; config 3, two rounds: 3.87 vs 3.83 ms)
+    // deferred pair outputs (DM 1) at two or more pair rounds when the frame's
+    // [P][K] scores fit next to the buffers: with the lagged four-pairs epilogue
+    // config 3 3.48 vs 3.50 ms per step, config 4 90.1 vs 95.0 (round 5; with
+    // the round-4 epilogue config 3 had measured 3.87 vs 3.83, in-round faster)
     constexpr int P = M * (M - 1) / 2, G = 16384 / C, ROUNDS = (P + G - 1) / G;
     // TDOA_F16_DEFER=0 / 1 forces a mode
     static const int force = [] {
@@ -1717,7 +1718,8 @@ static bool frame16_defer(const tdoa_kparams &kp)
         return e ? atoi(e) : -1;
     }();
     const size_t lds_defer = frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float);
-    return (force >= 0 ? force == 1 : ROUNDS >= 3) && lds_defer <= 160 * 1024;
+    constexpr int MIN_ROUNDS = (F16_OUT16 && F16_EPI_LAG) ? 2 : 3;
+    return (force >= 0 ? force == 1 : ROUNDS >= MIN_ROUNDS) && lds_defer <= 160 * 1024;
 }
 template <int C, int M>
 static bool frame16_fg(const tdoa_kparams &kp)

@@ -3,7 +3,8 @@
 oracle (oracle/gcc_phat_oracle.py) with test_gpu_gcc_phat.py's tolerances:
 
   TDOA_F16=w          k_frame16w, one wave per pair (config 4's shape)
-  TDOA_F16_DEFER=0    k_frame16 with every pair's outputs in its round
+  TDOA_F16_DEFER=0    k_frame16 with every pair's outputs in its round (config 3
+                      and 4 shapes)
   TDOA_F16_DEFER=1    k_frame16 with the deferred per-frame epilogue (at
                       C = 4096 the window table leaves no LDS for it: in-round)
   TDOA_F16_FG=1       the grid solved inside k_frame16 by the last pair round's
@@ -14,7 +15,7 @@ oracle (oracle/gcc_phat_oracle.py) with test_gpu_gcc_phat.py's tolerances:
 Every case also checks the cell / max_Lf bit for bit against the exhaustive
 float32 scan of the run's own weighted scores (vga_heatmap.h:99-108).
 
-The defaults (k_frame16, deferred at config 4, in-round at config 3) run in
+The defaults (k_frame16, deferred lagged epilogue at configs 3 and 4) run in
 test_gpu_gcc_phat.py itself.
 """
 import os
@@ -59,6 +60,7 @@ print("variant ok", ph.batch_kernel())
 @pytest.mark.parametrize("env,M,N", [
     ({"TDOA_F16": "w"}, 8, 2048),
     ({"TDOA_F16_DEFER": "0"}, 8, 2048),
+    ({"TDOA_F16_DEFER": "0"}, 4, 4096),  # config 3 with in-round outputs
     ({"TDOA_F16_DEFER": "1"}, 4, 2048),  # one pair round, epilogue forced
     ({"TDOA_F16_FG": "1"}, 8, 2048),  # config 4, deferred epilogue: one score buffer
     ({"TDOA_F16_FG": "1"}, 4, 4096),  # config 3 with the fused grid (in-round outputs)

@@ -59,7 +59,7 @@ else:
     names = ["start", "fw dc", "fw p1", "fw p2 dft", "fw p2 wr", "fw p3 dft", "fw p3 wr", "forward",
              "U regs"] + sum([[f"r{r} Y", f"r{r} p1 dft", f"r{r} p1 wr", f"r{r} p2 dft",
                                                    f"r{r} p2 wr", f"r{r} p3"] for r in range(R)], [])
-    dm = os.environ.get("TDOA_F16_DEFER", "1" if R >= 3 else "0")
+    dm = os.environ.get("TDOA_F16_DEFER", "1" if R >= 2 else "0")
     if dm == "1":
         names.append("epilogue")  # the deferred pair outputs (DM 1)
 n = len(names)
