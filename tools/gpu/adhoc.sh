@@ -1,4 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/bif3a gpurun_out/bif3b
-TAG=bif3a STEPS=5 BENCH_ARGS="--no-parity" tools/gpu/run.sh kstats:4 && \
-TDOA_NO_FRAME_BOUNDS=1 TAG=bif3b STEPS=5 BENCH_ARGS="--no-parity" tools/gpu/run.sh kstats:4
+export TAG=m6
+mkdir -p gpurun_out/$TAG
+tools/gpu/run.sh bench:3 bench:4 bench:2 bench:5:direct && \
+tools/gpu/run.sh kstats:3 kstats:4 pmc:3 pmc:4
