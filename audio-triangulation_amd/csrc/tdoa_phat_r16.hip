@@ -126,6 +126,14 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_EPI_LAG
 #define F16_EPI_LAG 1
 #endif
+// a barrier between the split (unit spectra) and the first round's Y stores
+#ifndef F16_SPLIT_BAR
+#define F16_SPLIT_BAR 0
+#endif
+// a barrier between the forward's pass-3 reads and its stores
+#ifndef F16_P3_BAR
+#define F16_P3_BAR 0
+#endif
 // timing only (A/B builds): no per-pair outputs at all (lags, compact scores, grid
 // inputs wrong) -- what the output stage costs
 #ifndef F16_NO_OUT
@@ -719,7 +727,11 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             v[r] = c_mul(v[r], c_mul(F16_LD(tt + 256 + 16 * r + (j & 15)), F16_LD(tt + 512 + 16 * r + (j >> 4))));  // twC
 #endif
         dftp<16, false, false>(v);
+        // the pass's stores go to exactly the 16 positions this thread read (its
+        // column): no barrier between the reads and the stores (F16_P3_BAR=1: one)
+#if F16_P3_BAR
         __syncthreads();
+#endif
     mark();
 #pragma unroll
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
@@ -1384,7 +1396,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         const f2 zh = bufs[tid * BUF + lidx<XS>(C / 2)];
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
     }
+    // No barrier before the first round's Y stores (F16_SPLIT_BAR=0): a thread
+    // stores Y only at the positions it has just read (bins b and C - b of every
+    // slot), and position C / 2 -- read for X[C/2] by threads 0 .. M - 1, stored
+    // by thread 0 -- stays inside wave 0, whose LDS operations are in order
+#if F16_SPLIT_BAR
     __syncthreads();  // slots consumed: they become the pairs' buffers
+#endif
     if (fr == diag_fr)
         F16_MARK();  // unit spectra in registers
     {
