@@ -1515,17 +1515,27 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             if (!on && fgr)
                 fgk = fgg.candidate(pgw, gw, gln, fgc);  // seg C
         }
-        __syncthreads();
+        // XS: the four outputs go to this thread's own column rows 0-3 (element
+        // jl + T c for output c), positions no other thread reads in this pass:
+        // no barrier between the pass's reads and its stores.  Padded layout:
+        // element 64 a + 16 c + k (a = jl >> 4), after a barrier
+        if constexpr (!XS)
+            __syncthreads();
         if (fr == diag_fr)
             F16_MARK();
         if (on) {
-            // element 64 a + 16 c + k (a = jl >> 4, c < 4): pidx = pidx(64 a + k) + 17 c;
-            // xs = (64 a | (k ^ (4 a & 15))) ^ 17 c
-            const int o = XS ? (64 * (jl >> 4) | (k ^ (4 * (jl >> 4) & 15))) : pidx((jl >> 4) * 64 + k);
-            buf[o] = x0;
-            buf[XS ? o ^ 17 : o + 17] = x1;
-            buf[XS ? o ^ 34 : o + 34] = x14;
-            buf[XS ? o ^ 51 : o + 51] = x15;
+            if constexpr (XS) {
+                buf[cjl.at(0)] = x0;
+                buf[cjl.at(1)] = x1;
+                buf[cjl.at(2)] = x14;
+                buf[cjl.at(3)] = x15;
+            } else {
+                const int o = pidx((jl >> 4) * 64 + k);
+                buf[o] = x0;
+                buf[o + 17] = x1;
+                buf[o + 34] = x14;
+                buf[o + 51] = x15;
+            }
         }
         if constexpr (FGL) {
             if (!on && fgr && gln == 0) {  // seg D
@@ -1547,15 +1557,21 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             const int mm = 64 - l;
             // column 192 + l (l >= 32): W_C^{-r (192 + l)} term == W_C^{r (64 - l)} after
             // the output index C - m; tw3 holds each lane's factors (conjugated for l < 32)
-            // element l + 64 r: pidx = pidx(l) + 68 r; xs = (xs(l) ^ 4 (r & 3)) + 64 r
+            // term r of lane l = 16 c + k: output c of pass-2 thread 16 r + k.  XS:
+            // element 16 r + k + T c, xs = (T c + 16 r) | (k ^ ((r + (T / 16) c) & 15));
+            // padded: element l + 64 r, pidx = pidx(l) + 68 r
             const int pl = lidx<XS>(l);
+            const int c3 = l >> 4, k3 = l & 15;
+            auto p3pos = [&](int r) {
+                return XS ? ((T * c3 + 16 * r) | (k3 ^ ((r + (T / 16) * c3) & 15))) : pl + 68 * r;
+            };
             // the R1 terms summed as a tree (a running sum was a dependent
             // chain of R1 - 1 complex products and adds on the round's critical path)
             f2 t[R1];
-            t[0] = F16_LD(buf + pl);
+            t[0] = F16_LD(buf + p3pos(0));
 #pragma unroll
             for (int r = 1; r < R1; r++)
-                t[r] = c_mul(F16_LD(buf + (XS ? (pl ^ (4 * (r & 3))) + 64 * r : pl + 68 * r)), F16_LD(tw3 + 64 * r + l));
+                t[r] = c_mul(F16_LD(buf + p3pos(r)), F16_LD(tw3 + 64 * r + l));
 #pragma unroll
             for (int h = R1 / 2; h >= 1; h >>= 1)
 #pragma unroll
