@@ -126,6 +126,13 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_EPI_LAG
 #define F16_EPI_LAG 1
 #endif
+// lagged epilogue: the first F16_EPI_SPLIT output waves run after the forward's
+// pass-2 stores, the rest after its pass-3 stores (-1: half).  Default 0, all
+// after pass 3: half and half measured slower (config 4 90.4 vs 88.5 ms per
+// step, config 3 3.57 vs 3.42 -- the pass-2 interval feeds pass 3's VALU-bound DFT)
+#ifndef F16_EPI_SPLIT
+#define F16_EPI_SPLIT 0
+#endif
 // a barrier between the split (unit spectra) and the first round's Y stores
 #ifndef F16_SPLIT_BAR
 #define F16_SPLIT_BAR 0
@@ -601,10 +608,11 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 // WM: where the thread's window words come from -- 0 global (L2), 1 LDS (win
 // is the LDS copy), 2 registers (wr, loaded once per launch)
 struct NoHook16 {
-    __device__ void operator()() const {}
+    __device__ void operator()(int) const {}
 };
-// hook: called once every thread's pass-3 stores are issued, before the
-// closing barrier (an LDS-store-bound interval whose VALU is idle):
+// hook(2) / hook(3): called once every thread's pass-2 / pass-3 stores are
+// issued, before the pass's closing barrier (LDS-store-bound intervals whose
+// VALU is idle):
 // k_frame16's lagged epilogue runs the previous frame's outputs there
 template <int C, int WM, typename Mark, bool XS = false, typename Hook = NoHook16>
 __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, const uint32_t (&wr)[8],
@@ -701,6 +709,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             buf[XS ? (lv ^ cr) : o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
         }
     }
+    hook(2);
     __syncthreads();
     mark();
     {
@@ -737,7 +746,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
             buf[XS ? cj.at(q) : pj + po(T * q)] = v[brev<16>(q)];
     }
-    hook();
+    hook(3);
     __syncthreads();
     mark();
 }
@@ -1249,10 +1258,14 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // DM 1 (four-pairs epilogue), lagged (F16_EPI_LAG): frame f's outputs run in
     // frame f + 1's forward, after its pass-3 stores; its gate after that forward
     constexpr bool ELAG = OUT16 && F16_EPI_LAG != 0;
-    auto epi16 = [&](int64_t f) {
+    // the waves (four pairs each) whose outputs run after the forward's pass-2
+    // stores; the rest after its pass-3 stores (F16_EPI_SPLIT: -1 half, else count)
+    constexpr int EPW = (P + 3) / 4, EPS = F16_EPI_SPLIT < 0 ? EPW / 2 : (F16_EPI_SPLIT < EPW ? F16_EPI_SPLIT : EPW);
+    auto epi16 = [&](int64_t f, int ps) {
         const int t = opaque_idx((int)threadIdx.x);
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = t >> 4;
-        if (!F16_NO_OUT && 4 * wv < P && pe < P) {
+        const bool mine = ps == 0 || (ps == 2 ? wv < EPS : wv >= EPS);
+        if (!F16_NO_OUT && mine && 4 * wv < P && pe < P) {
             const int r = t & 15, lo = (int)(e16_rng & 0xFFu), wd = (int)((e16_rng >> 8) & 0xFFu),
                       of = (int)(e16_rng >> 16);
             if (kp.K <= 96)
@@ -1349,9 +1362,9 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             F16_MARK();  // the forward's barriers (diagnostic build)
     };
     if constexpr (ELAG) {
-        auto lag_hook = [&] {
+        auto lag_hook = [&](int ps) {
             if (prev >= 0)
-                epi16(prev);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
+                epi16(prev, ps);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
         };
         frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS, decltype(lag_hook)>(
             w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N, fwd_mark, lag_hook);
@@ -1622,7 +1635,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             // ELAG: in the next frame's forward (or after the loop) instead
             if constexpr (!ELAG) {
                 pin_words();
-                epi16(fr);
+                epi16(fr, 0);
             }
         } else {
         const bool oka = ln < K, okb = ln + 64 < K;
@@ -1660,7 +1673,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     if constexpr (ELAG) {
         // the last frame's outputs (its last round closed with a barrier: scl complete)
         if (prev >= 0) {
-            epi16(prev);
+            epi16(prev, 0);
             __syncthreads();
             gate_of(prev);
         }
