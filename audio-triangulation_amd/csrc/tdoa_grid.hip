@@ -163,8 +163,15 @@ __device__ unsigned long long g_diag_bb[8192 * 8];  // per-wave phase cycles (td
 // ---------------------------------------------------------------------------
 // k_grid_bb: the same solve (max L, first argmax tuple) by exact branch and
 // bound, one wave per frame (tdoa_grid_bb.h).
+// at most 10 waves (640 threads) for the many-pair tables (TWC > 4, more than 8
+// pairs: config 4's LDS holds 10 frames), so the solve gets up to 168 VGPRs
+// instead of 128
+template <int TWC> constexpr int bb_max_threads() { return TWC > 4 ? 640 : 1024; }
+#ifndef BB_WPE
+#define BB_WPE
+#endif
 template <typename T, int TWC, int JT>
-__global__ void __launch_bounds__(1024) k_grid_bb(tdoa_kparams kp, tdoa_kout out,
+__global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_kparams kp, tdoa_kout out,
                                                   const T *__restrict__ weighted, int64_t B)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -314,7 +321,7 @@ int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, i
     const size_t per_wave =
         (((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 15) & ~(size_t)15;
     int nw = (int)((BB_LDS - table) / per_wave);
-    nw = nw > 16 ? 16 : nw;
+    nw = nw > bb_max_threads<TWC>() / 64 ? bb_max_threads<TWC>() / 64 : nw;
     const size_t lds = table + (size_t)nw * per_wave;
     const void *kern = (const void *)k_grid_bb<T, TWC, JT>;
     const int res = tdoa_resident_blocks(kern, nw * 64, lds);
@@ -411,6 +418,8 @@ int launch(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int6
     if (bb_fits<T>(kp)) {
         if (kp.TW == 1)
             launch_bb_jt<T, 1>(kp, out, weighted, B, st);
+        else if (kp.TW == 2)  // 5-8 pairs: up to 16 waves per workgroup
+            launch_bb_jt<T, 2>(kp, out, weighted, B, st);
         else
             launch_bb_jt<T, TWX>(kp, out, weighted, B, st);
         hipError_t e = hipGetLastError();

@@ -25,6 +25,11 @@
 #include "tdoa_fft32.h"
 #include "tdoa_internal.h"
 
+// many pairs, P % 4 == 0: the bounds' queries unguarded (see solve_wave)
+#ifndef BB_Q4
+#define BB_Q4 1
+#endif
+
 namespace tdoa_bb {
 
 // diagnostic build only (TDOA_DIAG): s_memtime cycles per phase accumulated
@@ -171,7 +176,9 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
 #pragma unroll
     for (int j = 0; j < JT; j++)
         bt[j] = (lane + 64 * j < NT) ? (T)0 : low;
-    if (P <= 8) {
+    // TWC <= 2 instantiations take TW <= 2 tables (P <= 8, tdoa_grid.hip), the
+    // others P > 8: one path per instantiation
+    if constexpr (TWC <= 2) {
         // few pairs: levels 1, 2, 3 of every pair in three wave-synced passes
         // (the range loop they replace issued n dependent reads per range: 69 %
         // of a config-3 wave)
@@ -186,6 +193,33 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
         for (int i = lane; i < PK; i += 64)
             S8[i] = vmax<T>(S4[i], S4[i + 4 < PK ? i + 4 : i]);
         wave_lds_sync();
+#if BB_Q4
+        if (NT > 0) {
+            // every lane and pair slot reads (entry clamped to NT - 1, pair to
+            // P - 1), an entry's windows all before its first max; the sum
+            // takes p < P
+#pragma unroll
+            for (int j = 0; j < JT; j++) {
+                T wa[8], wb[8];
+                const int t = lane + 64 * j < NT ? lane + 64 * j : NT - 1;
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    const uint32_t q = qt[t * P + (p < P ? p : P - 1)];
+                    const int o1 = (int)(q & 0x1FFFu), dl = (int)(q >> 13);
+                    wa[p] = Wl[o1];
+                    wb[p] = Wl[o1 + dl];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                T b = 0;
+#pragma unroll
+                for (int p = 0; p < 8; p++)
+                    if (p < P)  // bounds summed in L's own pair order
+                        b += vmax<T>(wa[p], wb[p]);
+                bt[j] = lane + 64 * j < NT ? b : low;
+            }
+        }
+        if (false)
+#endif
 #pragma unroll
         for (int j = 0; j < JT; j++) {
             const int t = lane + 64 * j;
@@ -213,6 +247,26 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
         // per config-4 frame against 1.87 with exact ones
         const int RW = bb_row(K), gq = lane >> 4, q8 = 8 * (lane & 15);
         T *G = Wl + PKp;  // [3][4][RW]
+#if BB_Q4
+        // P % 4 == 0: every lane queries (lanes past NT repeat entry NT - 1 and
+        // are masked after the loop), with no per-pair guard, so a group's
+        // query words and range reads issue together instead of one pair's
+        // round trip after another; the next group's words are requested a
+        // group ahead
+        const bool q4 = (P & 3) == 0 && NT > 0;
+        int tq[JT];
+#pragma unroll
+        for (int j = 0; j < JT; j++)
+            tq[j] = lane + 64 * j < NT ? lane + 64 * j : NT - 1;
+        uint2 qn[JT];
+        if (q4) {
+#pragma unroll
+            for (int j = 0; j < JT; j++) {
+                qn[j] = *reinterpret_cast<const uint2 *>(qt + tq[j] * P);
+                bt[j] = (T)0;
+            }
+        }
+#endif
         for (int p0 = 0; p0 < P; p0 += 4) {
             wave_lds_sync();  // the previous group's level reads come first
             if (p0 + gq < P && q8 < RW) {
@@ -243,6 +297,36 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
                     dst[8 * RW + d] = x[d];
             }
             wave_lds_sync();
+#if BB_Q4
+            if (q4) {
+                uint2 qc[JT];
+#pragma unroll
+                for (int j = 0; j < JT; j++) {
+                    qc[j] = qn[j];
+                    if (p0 + 4 < P)
+                        qn[j] = *reinterpret_cast<const uint2 *>(qt + tq[j] * P + p0 + 4);
+                }
+                // every window read issued before the first max (the scheduler
+                // otherwise waits on each range's two reads in turn)
+                T wa[JT][4], wb[JT][4];
+#pragma unroll
+                for (int j = 0; j < JT; j++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const uint32_t q = ((g < 2 ? qc[j].x : qc[j].y) >> (16 * (g & 1))) & 0xFFFFu;
+                        const int o1 = (int)(q & 0x1FFFu), dl = (int)(q >> 13);
+                        wa[j][g] = Wl[o1];
+                        wb[j][g] = Wl[o1 + dl];
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < JT; j++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++)  // bounds summed in L's own pair order
+                        bt[j] += vmax<T>(wa[j][g], wb[j][g]);
+                continue;
+            }
+#endif
 #pragma unroll
             for (int j = 0; j < JT; j++) {
                 const int t = lane + 64 * j;
@@ -272,6 +356,13 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
                 }
             }
         }
+#if BB_Q4
+        if (q4)
+#pragma unroll
+            for (int j = 0; j < JT; j++)
+                if (lane + 64 * j >= NT)
+                    bt[j] = low;
+#endif
     }
     BB_MARK(1);
     // seed: the entry of largest bound (first on ties; NaN bounds never win)
