@@ -329,10 +329,11 @@ uint16_t bb_query(int P, int K, int p, int lo, int hi)
     if (n > 15)
         return 0x1FFF;  // wide: the table is not used (kp.bb_wide)
     const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
-    const int PKp = (P * K + 3) & ~3, RW = K <= 96 ? 96 : 128;
+    const int KS = P > 8 ? (K + 3) & ~3 : K;  // bb_ks (tdoa_grid_bb.h): score row stride
+    const int PKp = (P * KS + 3) & ~3, RW = K <= 96 ? 96 : 128;
     int o1;
     if (lv == 0)
-        o1 = p * K + lo;  // the scores themselves
+        o1 = p * KS + lo;  // the scores themselves
     else if (P <= 8)
         o1 = lv * PKp + p * K + lo;  // levels [3][P][K] after the scores
     else
@@ -744,7 +745,12 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
         int off = 0;
         bool ok = c->P <= TDOA_MAX_PAIRS;
         c->wc_chunks.clear();
+        // many pairs (P > 8): k_grid_bb's score rows are KS = bb_ks apart and a
+        // range starts at a multiple of 4 lags, so every chunk lands 16-B aligned
+        const int KS = c->P > 8 ? (c->K + 3) & ~3 : c->K;
         for (int p = 0; ok && p < c->P; p++) {
+            if (c->P > 8 && hi[p] >= lo[p])
+                lo[p] &= ~3;
             const int w = hi[p] - lo[p] + 1;
             ok = w > 0 && off < 65536;
             if (!ok)
@@ -753,7 +759,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             kp.wc_w[p] = (uint8_t)w;
             kp.wc_off[p] = (uint16_t)off;
             for (int j = 0; j < w; j += 4)
-                c->wc_chunks.push_back((uint32_t)(p * c->K + lo[p] + j) | ((uint32_t)std::min(4, w - j) << 16));
+                c->wc_chunks.push_back((uint32_t)(p * KS + lo[p] + j) | ((uint32_t)std::min(4, w - j) << 16));
             off += (w + 3) & ~3;
         }
         if (ok && hipMalloc(&c->d_wc, c->wc_chunks.size() * 4) == hipSuccess &&

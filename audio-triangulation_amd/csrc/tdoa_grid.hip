@@ -175,17 +175,15 @@ __global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_k
                                                   const T *__restrict__ weighted, int64_t B)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int P = kp.P, K = kp.K, NT = kp.bb_NT, PK = P * K;
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, PK = P * K, KS = tdoa_bb::bb_ks(P, K);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NW = blockDim.x >> 6;
-    int32_t *tiles = (int32_t *)smem;                                         // [NT][2]
-    uint16_t *qt = (uint16_t *)(smem + (size_t)NT * 8);                       // [NT][P]
+    const int32_t *tiles = kp.bb_tile;  // [NT][2], read by entry (wave-uniform)
+    uint16_t *qt = (uint16_t *)smem;    // [NT][P]
     // per wave: the frame's scores Wl [P][K], then the solve's sparse-table
     // levels (tdoa_bb::bb_scratch), 16-B aligned
     const size_t per_wave =
         ((size_t)(tdoa_bb::bb_pk(P, K) + tdoa_bb::bb_scratch(P, K)) * sizeof(T) + 15) & ~(size_t)15;
-    T *Wl = (T *)(smem + (((size_t)NT * (8 + 2 * P)) + 15 & ~(size_t)15) + (size_t)wave * per_wave);
-    for (int e = tid; e < 2 * NT; e += blockDim.x)
-        tiles[e] = kp.bb_tile[e];
+    T *Wl = (T *)(smem + (((size_t)NT * 2 * P) + 15 & ~(size_t)15) + (size_t)wave * per_wave);
     for (int e = tid; e < NT * P; e += blockDim.x)
         qt[e] = kp.bb_q[e];
     __syncthreads();
@@ -193,7 +191,7 @@ __global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_k
     unsigned long long bbacc[8] = {};
     if constexpr (std::is_same<T, float>::value)
         if (out.weighted_c)  // compact scratch: the unused lags of Wl stay defined (never read)
-            for (int e = lane; e < PK; e += 64)
+            for (int e = lane; e < tdoa_bb::bb_pk(P, K); e += 64)
                 Wl[e] = (T)0;
     for (int64_t f = (int64_t)blockIdx.x * NW + wave; f < B; f += (int64_t)gridDim.x * NW) {
 #ifdef TDOA_DIAG
@@ -211,7 +209,7 @@ __global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_k
                 compact = out.weighted_c != nullptr;
             if (compact) {
                 // compact scratch: 16-B chunks of the used lags, expanded to
-                // Wl[p][K] (lags no tuple uses are never read)
+                // Wl[p][KS] (lags no tuple uses are never read)
                 typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
                 const v4u_t *s4 = reinterpret_cast<const v4u_t *>(out.weighted_c + f * kp.wc_CK);
                 const int nch = kp.wc_nch;
@@ -228,7 +226,12 @@ __global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_k
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const int c = b + i * 64 + lane;
-                        if (c < nch) {
+                        if (c < nch && P > 8) {
+                            // many pairs: 16-B aligned chunks (rows KS apart, chunk
+                            // starts multiples of 4, tdoa_capi.cpp): one store; a
+                            // last chunk's extra lags lie past every tuple's lag
+                            *reinterpret_cast<v4u_t *>(reinterpret_cast<float *>(Wl) + (dsc[i] & 0xFFFFu)) = t[i];
+                        } else if (c < nch) {
                             float *d = reinterpret_cast<float *>(Wl) + (dsc[i] & 0xFFFFu);
                             const int n = (int)(dsc[i] >> 16);
                             // scalar copies first: __builtin_bit_cast of an
@@ -244,6 +247,11 @@ __global__ void __launch_bounds__(bb_max_threads<TWC>()) BB_WPE k_grid_bb(tdoa_k
                         }
                     }
                 }
+            } else if (KS != K) {
+                // full [P][K] scores into rows KS apart
+                const T *src = weighted + f * PK;
+                for (int e = lane; e < PK; e += 64)
+                    Wl[e + (e / K) * (KS - K)] = __builtin_nontemporal_load(&src[e]);
             } else {
             const T *src = weighted + f * PK;
             const int nv = (int)(((size_t)PK * sizeof(T)) / 16);
@@ -317,7 +325,7 @@ template <typename T, int TWC, int JT>
 int launch_bb(const tdoa_kparams &kp, const tdoa_kout &out, const T *weighted, int64_t B,
               hipStream_t st)
 {
-    const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
+    const size_t table = ((size_t)kp.bb_NT * 2 * kp.P + 15) & ~(size_t)15;  // the queries
     const size_t per_wave =
         (((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 15) & ~(size_t)15;
     int nw = (int)((BB_LDS - table) / per_wave);
@@ -352,7 +360,7 @@ bool bb_fits(const tdoa_kparams &kp)
 {
     if (kp.bb_NT <= 0 || kp.bb_NT > 256 || !kp.bb_tile || !kp.bb_q || kp.bb_wide)
         return false;
-    const size_t table = ((size_t)kp.bb_NT * (8 + 2 * kp.P) + 15) & ~(size_t)15;
+    const size_t table = ((size_t)kp.bb_NT * 2 * kp.P + 15) & ~(size_t)15;  // the queries
     return kp.K <= 127 &&
            table + ((size_t)tdoa_bb::bb_pk(kp.P, kp.K) + tdoa_bb::bb_scratch(kp.P, kp.K)) * sizeof(T) + 16 <= BB_LDS;
 }

@@ -131,8 +131,12 @@ __device__ __forceinline__ void wave_best(T &v, int &i)
 
 // row stride of the grouped levels (P > 8): 8 lags per lane, 12 or 16 lanes
 __host__ __device__ constexpr int bb_row(int K) { return K <= 96 ? 96 : 128; }
+// row stride of the frame's scores in LDS: K, or K rounded up to 16 B for many
+// pairs (P > 8), whose level build then reads a lane's 16 scores as four
+// aligned 16-B reads and whose compact chunks expand by one 16-B store each
+__host__ __device__ constexpr int bb_ks(int P, int K) { return P > 8 ? (K + 3) & ~3 : K; }
 // the frame's scores per wave, padded to 16 B: the levels follow them
-__host__ __device__ constexpr int bb_pk(int P, int K) { return (P * K + 3) & ~3; }
+__host__ __device__ constexpr int bb_pk(int P, int K) { return (P * bb_ks(P, K) + 3) & ~3; }
 
 // LDS scratch elements per wave after the frame's scores: the sparse table's
 // levels 1, 2, 3 [3][P][K] (P <= 8, bb_pk apart), or the same levels of four
@@ -156,10 +160,10 @@ __device__ __forceinline__ T bb_range_max(const T *Wl, uint32_t q)
     return vmax<T>(Wl[o1], Wl[o1 + dl]);
 }
 
-// One frame, one wave.  Wl: the frame's weighted scores [P][K] in LDS (written
+// One frame, one wave.  Wl: the frame's weighted scores [P][KS] in LDS (written
 // by this wave before the call), followed by bb_scratch(P, K) scratch
 // elements (16-B aligned); qt: the entries' range queries [NT][P];
-// tiles: the entry table (LDS or global).  Returns the max L (best) and
+// tiles: the entry table (global: an entry index is wave-uniform).  Returns the max L (best) and
 // its tuple index in first-cell order (bu, INT_MAX when no L exceeded the
 // lowest value).  Every lane returns the same pair.
 template <typename T, int TWC, int JT>
@@ -169,7 +173,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
 {
     (void)bbacc;
     BB_T0();
-    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW, PKp = bb_pk(P, K);
+    const int P = kp.P, K = kp.K, NT = kp.bb_NT, TW = kp.TW, PKp = bb_pk(P, K), KS = bb_ks(P, K);
     const T low = lowest<T>();
     // entry bounds, lane-strided, in L's own pair order
     T bt[JT];
@@ -270,11 +274,18 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
         for (int p0 = 0; p0 < P; p0 += 4) {
             wave_lds_sync();  // the previous group's level reads come first
             if (p0 + gq < P && q8 < RW) {
-                const T *w = Wl + (p0 + gq) * K;
-                T x[15];
+                const T *w = Wl + (p0 + gq) * KS;
+                T x[16];
+                // lags q8 .. q8 + 15 as aligned 16-B reads (KS and q8 multiples
+                // of 4; past the row's K lags they read the next row or the
+                // levels: windows there are never queried, a query's windows lie
+                // inside its range)
+                constexpr int PER = 16 / (int)sizeof(T);
 #pragma unroll
-                for (int d = 0; d < 15; d++)
-                    x[d] = w[q8 + d < K ? q8 + d : K - 1];
+                for (int v = 0; v < 16 / PER; v++) {
+                    const uint4 u = *reinterpret_cast<const uint4 *>(w + q8 + v * PER);
+                    __builtin_memcpy(&x[v * PER], &u, 16);
+                }
                 // in place, each level stored as soon as it is built (few live values)
                 T *dst = G + gq * RW + q8;
 #pragma unroll
@@ -412,7 +423,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
                     for (int b = 0; b < 4; b++) {
                         const int p = 4 * tw + b;
                         if (p < P)
-                            L += Wl[p * K + ((pr.w[tw] >> (8 * b)) & 0xFFu)];
+                            L += Wl[p * KS + ((pr.w[tw] >> (8 * b)) & 0xFFu)];
                     }
                 }
             }
