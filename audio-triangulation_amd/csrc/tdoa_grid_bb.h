@@ -29,6 +29,10 @@
 #ifndef BB_Q4
 #define BB_Q4 1
 #endif
+// the evaluations' loads and gathers unguarded (see solve_wave)
+#ifndef BB_EV
+#define BB_EV 1
+#endif
 
 namespace tdoa_bb {
 
@@ -398,6 +402,41 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
         uint32_t w[TWC];
         int ui, cnt;
     };
+#if BB_EV
+    // unguarded: the entry's (start, count) as one uniform load, every lane's
+    // words and index requested at once (lanes past the count load the
+    // entry's first tuple; their L is masked), and every gather issued before
+    // the first add -- guarded, each load or gather was its own round trip
+    auto fetch = [&](int t, Pre &pr) {
+        const int2 tc = *reinterpret_cast<const int2 *>(tiles + 2 * t);
+        pr.cnt = tc.y;
+        const int u = tc.x + (lane < tc.y ? lane : 0);
+#pragma unroll
+        for (int tw = 0; tw < TWC; tw++)
+            pr.w[tw] = kp.bb_tuples[(size_t)u * TW + (tw < TW ? tw : TW - 1)];
+        const int ui = kp.bb_uidx[u];
+        pr.ui = lane < tc.y ? ui : INT_MAX;
+    };
+    auto consume = [&](const Pre &pr) {
+        BB_COUNT(4);
+        T g[4 * TWC];
+#pragma unroll
+        for (int p = 0; p < 4 * TWC; p++)  // pairs past P read row 0 (not summed)
+            g[p] = Wl[(p < P ? p * KS : 0) + ((pr.w[p >> 2] >> (8 * (p & 3))) & 0xFFu)];
+        __builtin_amdgcn_sched_barrier(0);
+        T L = 0;
+        if (P == 4 * TWC) {
+#pragma unroll
+            for (int p = 0; p < 4 * TWC; p++)
+                L += g[p];
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4 * TWC; p++)
+                if (p < P)
+                    L += g[p];
+        }
+        L = lane < pr.cnt ? L : low;
+#else
     auto fetch = [&](int t, Pre &pr) {
         const int start = tiles[2 * t];
         pr.cnt = tiles[2 * t + 1];
@@ -428,6 +467,7 @@ __device__ __forceinline__ void solve_wave(const tdoa_kparams &kp, T *Wl, const 
                 }
             }
         }
+#endif
         const int ui = pr.ui;
         const bool win = L > low && (L > best || (L == best && ui < bu));
         if (__ballot(win) == 0)

@@ -1,6 +1,6 @@
 set -o pipefail
-export TAG=g5
+export TAG=g7
 mkdir -p gpurun_out/$TAG
 tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py,tests/test_gpu_parity.py,tests/test_ls.py,tests/test_gpu_frame16_variants.py && \
-STEPS=8 BENCH_ARGS="--config 4" tools/gpu/run.sh ablib:libtdoa_gB,libtdoa,libtdoa_gB,libtdoa && \
-STEPS=60 BENCH_ARGS="--config 3" tools/gpu/run.sh ablib:libtdoa_gB,libtdoa
+STEPS=8 BENCH_ARGS="--config 4" tools/gpu/run.sh ablib:libtdoa_gC,libtdoa,libtdoa_gC,libtdoa && \
+STEPS=60 BENCH_ARGS="--config 3" tools/gpu/run.sh ablib:libtdoa_gC,libtdoa,libtdoa_gC,libtdoa
