@@ -340,14 +340,25 @@ __device__ __forceinline__ void lean_spectrum(const Lane &L, const uint32_t (&w)
 
 // real-FFT split of the partner pair k + unit normalisation: the unit
 // spectrum at bins b and N - b (the W_2048^b twiddle read next to its use)
-__device__ __forceinline__ void lean_split(const Lane &L, f2 A, f2 Bv, int k, float e2, f2 &ub,
-                                           f2 &un)
+__device__ __forceinline__ void lean_split_w(f2 A, f2 Bv, f2 wk, float e2, f2 &ub, f2 &un)
 {
-    const f2 wk = lds_f2(L.tw2, 8 * L.cs + 256 * k);
     const f2 e = c_addconj(A, Bv);
     const f2 od = c_mul(c_subconj(A, Bv), wk);
     ub = c_unit(c_add_mi(e, od), e2);
     un = c_unit(c_conj_add_i(e, od), e2);
+}
+// the W_2048^b twiddle of pair k (P1K_TWPF: requested one pair ahead of its
+// use, so its LDS round trip overlaps the previous pair's arithmetic; read
+// next to its use, each was a round trip of its own -- the inline-asm packed
+// operations keep the backend from hoisting it)
+#ifndef P1K_TWPF
+#define P1K_TWPF 1
+#endif
+__device__ __forceinline__ f2 lean_tw2(const Lane &L, int k) { return lds_f2(L.tw2, 8 * L.cs + 256 * k); }
+__device__ __forceinline__ void lean_split(const Lane &L, f2 A, f2 Bv, int k, float e2, f2 &ub,
+                                           f2 &un)
+{
+    lean_split_w(A, Bv, lean_tw2(L, k), e2, ub, un);
 }
 
 // unit spectrum of one mic row, in place (paired layout)
@@ -356,9 +367,20 @@ __device__ __forceinline__ void lean_forward(const Lane &L, const uint32_t (&w)[
                                              float e2, Hook after_front = Hook())
 {
     lean_spectrum(L, w, U, e2, after_front);
+#if P1K_TWPF
+    f2 wn = lean_tw2(L, 0);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const f2 wk = wn;
+        if (k < 15)
+            wn = lean_tw2(L, k + 1);
+        lean_split_w(U[k], U[31 - k], wk, e2, U[k], U[31 - k]);
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 16; k++)
         lean_split(L, U[k], U[31 - k], k, e2, U[k], U[31 - k]);
+#endif
 }
 
 // unit spectrum V of one mic row consumed bin pair by bin pair as it is
@@ -370,10 +392,20 @@ __device__ __forceinline__ void lean_forward_cross(const Lane &L, const uint32_t
     lean_spectrum(L, w, V, e2);
     A[32] = c_conjmul(A[32], V[32]);
     Bs[32] = c_conjmul(Bs[32], V[32]);
+#if P1K_TWPF
+    f2 wn = lean_tw2(L, 0);
+#endif
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         f2 ub, un;
+#if P1K_TWPF
+        const f2 wk = wn;
+        if (k < 15)
+            wn = lean_tw2(L, k + 1);
+        lean_split_w(V[k], V[31 - k], wk, e2, ub, un);
+#else
         lean_split(L, V[k], V[31 - k], k, e2, ub, un);
+#endif
         A[k] = c_conjmul(A[k], ub);
         A[31 - k] = c_conjmul(A[31 - k], un);
         Bs[k] = c_conjmul(Bs[k], ub);
@@ -450,11 +482,20 @@ template <bool CROSS>
 __device__ __forceinline__ void lean_pretwiddle(const Lane &L, const f2 (&A)[33], const f2 (&Bs)[33],
                                                 f2 (&v)[32])
 {
+#if P1K_TWPF
+    f2 wn = lean_tw2(L, 0);
+#endif
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const f2 Rk = CROSS ? c_conjmul(A[k], Bs[k]) : A[k];
         const f2 Rn = CROSS ? c_conjmul(A[31 - k], Bs[31 - k]) : A[31 - k];
-        const f2 wk = lds_f2(L.tw2, 8 * L.cs + 256 * k);
+#if P1K_TWPF
+        const f2 wk = wn;
+        if (k < 15)
+            wn = lean_tw2(L, k + 1);
+#else
+        const f2 wk = lean_tw2(L, k);
+#endif
         const f2 s = c_addconj(Rk, Rn);
         const f2 q = c_mulconj(c_subconj(Rk, Rn), wk);
         v[k] = c_add_i(s, q);

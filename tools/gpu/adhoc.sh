@@ -1,6 +1,5 @@
 set -o pipefail
-export TAG=e1
+export TAG=t1
 mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py,tests/test_ls.py,tests/test_gpu_frame16_variants.py && \
-STEPS=8 BENCH_ARGS="--config 4" tools/gpu/run.sh ablib:libtdoa_eA,libtdoa,libtdoa_eA,libtdoa && \
-STEPS=60 BENCH_ARGS="--config 3" tools/gpu/run.sh ablib:libtdoa_eA,libtdoa,libtdoa_eA,libtdoa
+tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py,tests/test_gpu_parity.py && \
+STEPS=400 tools/gpu/run.sh ablib:libtdoa_tw0,libtdoa,libtdoa_tw0,libtdoa,libtdoa_tw0,libtdoa
