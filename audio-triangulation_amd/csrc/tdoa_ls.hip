@@ -41,17 +41,28 @@ __global__ void __launch_bounds__(128) k_ls(tdoa_kparams kp, const T *__restrict
     constexpr int M = MM, P = MM * (MM - 1) / 2;
     const int K = kp.K;
     double tau[P];
+    if (peak3) {
+        // the sub-sample lags from the peaks' scores: every lag and peak word
+        // loaded before the first use (the branch inside the loop made each
+        // pair's loads a round trip of their own)
+        int best[P];
+        float y[3 * P];
 #pragma unroll
-    for (int p = 0; p < P; p++) {  // the sub-sample lags: from the peaks' scores or the raw scores
-        const int best = lags[f * P + p];
-        if (peak3) {
-            const float *y = peak3 + ((size_t)f * P + p) * 3;
-            const bool inside = best + K / 2 > 0 && best + K / 2 < K - 1;
-            tau[p] = inside ? ls_tau3((double)y[0], (double)y[1], (double)y[2], best, true)
-                            : ls_tau3(0.0, 0.0, 0.0, best, false);
-        } else {
-            tau[p] = ls_tau(scores + ((size_t)f * P + p) * K, K, best);
+        for (int p = 0; p < P; p++)
+            best[p] = lags[f * P + p];
+#pragma unroll
+        for (int e = 0; e < 3 * P; e++)
+            y[e] = peak3[(size_t)f * P * 3 + e];
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            const bool inside = best[p] + K / 2 > 0 && best[p] + K / 2 < K - 1;
+            tau[p] = inside ? ls_tau3((double)y[3 * p], (double)y[3 * p + 1], (double)y[3 * p + 2], best[p], true)
+                            : ls_tau3(0.0, 0.0, 0.0, best[p], false);
         }
+    } else {
+#pragma unroll
+        for (int p = 0; p < P; p++)  // ... or from the raw scores
+            tau[p] = ls_tau(scores + ((size_t)f * P + p) * K, K, lags[f * P + p]);
     }
     int cell = cells[f];
     cell = cell < 0 ? 0 : (cell >= kp.G ? kp.G - 1 : cell);
