@@ -352,7 +352,7 @@ __device__ __forceinline__ void lean_split_w(f2 A, f2 Bv, f2 wk, float e2, f2 &u
 // next to its use, each was a round trip of its own -- the inline-asm packed
 // operations keep the backend from hoisting it)
 #ifndef P1K_TWPF
-#define P1K_TWPF 1
+#define P1K_TWPF 5  // bit 0: lean_forward, 1: lean_forward_cross, 2: lean_pretwiddle
 #endif
 __device__ __forceinline__ f2 lean_tw2(const Lane &L, int k) { return lds_f2(L.tw2, 8 * L.cs + 256 * k); }
 __device__ __forceinline__ void lean_split(const Lane &L, f2 A, f2 Bv, int k, float e2, f2 &ub,
@@ -367,7 +367,7 @@ __device__ __forceinline__ void lean_forward(const Lane &L, const uint32_t (&w)[
                                              float e2, Hook after_front = Hook())
 {
     lean_spectrum(L, w, U, e2, after_front);
-#if P1K_TWPF
+#if P1K_TWPF & 1
     f2 wn = lean_tw2(L, 0);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -392,13 +392,13 @@ __device__ __forceinline__ void lean_forward_cross(const Lane &L, const uint32_t
     lean_spectrum(L, w, V, e2);
     A[32] = c_conjmul(A[32], V[32]);
     Bs[32] = c_conjmul(Bs[32], V[32]);
-#if P1K_TWPF
+#if P1K_TWPF & 2
     f2 wn = lean_tw2(L, 0);
 #endif
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         f2 ub, un;
-#if P1K_TWPF
+#if P1K_TWPF & 2
         const f2 wk = wn;
         if (k < 15)
             wn = lean_tw2(L, k + 1);
@@ -482,14 +482,14 @@ template <bool CROSS>
 __device__ __forceinline__ void lean_pretwiddle(const Lane &L, const f2 (&A)[33], const f2 (&Bs)[33],
                                                 f2 (&v)[32])
 {
-#if P1K_TWPF
+#if P1K_TWPF & 4
     f2 wn = lean_tw2(L, 0);
 #endif
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const f2 Rk = CROSS ? c_conjmul(A[k], Bs[k]) : A[k];
         const f2 Rn = CROSS ? c_conjmul(A[31 - k], Bs[31 - k]) : A[31 - k];
-#if P1K_TWPF
+#if P1K_TWPF & 4
         const f2 wk = wn;
         if (k < 15)
             wn = lean_tw2(L, k + 1);

@@ -1,5 +1,6 @@
 set -o pipefail
-mkdir -p gpurun_out/l1a gpurun_out/l1b
-tools/gpu/run.sh test:tests/test_ls.py,tests/test_gpu_bench_path.py && \
-TAG=l1a TDOA_LIB=$GRAFT_REPO_ROOT/audio-triangulation_amd/tdoa/libtdoa_lsA.so STEPS=10 tools/gpu/run.sh kstats:4 && \
-TAG=l1b STEPS=10 tools/gpu/run.sh kstats:4
+export TAG=t2
+mkdir -p gpurun_out/$TAG
+tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py && \
+STEPS=400 tools/gpu/run.sh ablib:libtdoa_tw0,libtdoa_tw7,libtdoa,libtdoa_tw0,libtdoa_tw7,libtdoa,libtdoa_tw0,libtdoa_tw7,libtdoa && \
+tools/gpu/run.sh pmc:2
