@@ -1,6 +1,6 @@
 set -o pipefail
-export TAG=t2
+export TAG=f1
 mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py && \
-STEPS=400 tools/gpu/run.sh ablib:libtdoa_tw0,libtdoa_tw7,libtdoa,libtdoa_tw0,libtdoa_tw7,libtdoa,libtdoa_tw0,libtdoa_tw7,libtdoa && \
-tools/gpu/run.sh pmc:2
+tools/gpu/run.sh test smoke && \
+tools/gpu/run.sh bench:2 bench:3 bench:4 bench:5:direct bench:2:direct bench:1 && \
+tools/gpu/run.sh kstats:2 kstats:3 kstats:4 kstats:5:direct
