@@ -1,6 +1,7 @@
 set -o pipefail
-export TAG=f1
-mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test smoke && \
-tools/gpu/run.sh bench:2 bench:3 bench:4 bench:5:direct bench:2:direct bench:1 && \
-tools/gpu/run.sh kstats:2 kstats:3 kstats:4 kstats:5:direct
+mkdir -p gpurun_out/w1a gpurun_out/w1b
+tools/gpu/run.sh test:tests/test_gpu_gcc_phat.py,tests/test_gpu_bench_path.py,tests/test_gpu_parity.py,tests/test_gpu_frame16_variants.py && \
+TAG=w1a TDOA_LIB=$GRAFT_REPO_ROOT/audio-triangulation_amd/tdoa/libtdoa_ws1.so STEPS=10 tools/gpu/run.sh kstats:4 && \
+TAG=w1b STEPS=10 tools/gpu/run.sh kstats:4 && \
+TAG=w1a TDOA_LIB=$GRAFT_REPO_ROOT/audio-triangulation_amd/tdoa/libtdoa_ws1.so STEPS=60 tools/gpu/run.sh kstats:3 && \
+TAG=w1b STEPS=60 tools/gpu/run.sh kstats:3
