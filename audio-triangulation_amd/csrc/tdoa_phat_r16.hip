@@ -130,6 +130,11 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 // pass-2 stores, the rest after its pass-3 stores (-1: half).  Default 0, all
 // after pass 3: half and half measured slower (config 4 90.4 vs 88.5 ms per
 // step, config 3 3.57 vs 3.42 -- the pass-2 interval feeds pass 3's VALU-bound DFT)
+#ifndef F16_OUT16_LOOPS
+// frame16_out16: a loop per output kind under its pointer test (0: one loop
+// with the tests inside; config 3 1.925e7 -> 1.967e7, config 4 equal)
+#define F16_OUT16_LOOPS 1
+#endif
 #ifndef F16_EPI_SPLIT
 #define F16_EPI_SPLIT 0
 #endif
@@ -883,7 +888,7 @@ __device__ __forceinline__ void frame16_pair_out(const tdoa_kparams &kp, const t
 // frame, was the epilogue's cost.  Same values, same tie rule (ascending lags
 // per lane with a strict '>', then the smallest lag among equal keys), same
 // stores.  wlo, ww, woff: this lane's pair's compact-scratch range.
-template <int KL>
+template <int KL, bool SPLIT = (F16_OUT16_LOOPS != 0)>
 __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa_kout &out, const float *scl,
                                               const float *priorl, int *lagl, int64_t fr, int P, int p, int r,
                                               int wlo, int ww, int woff)
@@ -908,6 +913,45 @@ __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa
     float *wc = kernarg_out()->weighted_c;
     float *pk3 = kernarg_out()->peak3;
     float *wcp = wc ? wc + (size_t)fr * kp.wc_CK + woff - wlo : nullptr;
+#if F16_OUT16_LOOPS
+    if constexpr (SPLIT) {
+    // one loop per output kind under its (uniform) pointer test: inside one
+    // loop, every lag re-derived each test's lane mask (VALU) and branched
+    if (out.scores_f)
+#pragma unroll
+        for (int i = 0; i < KL; i++)
+            if (r + 16 * i < K)
+                out.scores_f[gb + r + 16 * i] = sv[i];
+    if (out.weighted_f || wcp) {
+        float wv[KL];
+#pragma unroll
+        for (int i = 0; i < KL; i++) {
+            const int k = r + 16 * i;
+            wv[i] = k < K ? sv[i] * priorl[k > b ? k - b : b - k] : 0.0f;
+        }
+        if (out.weighted_f)
+#pragma unroll
+            for (int i = 0; i < KL; i++)
+                if (r + 16 * i < K)
+                    out.weighted_f[gb + r + 16 * i] = wv[i];
+        if (wcp)
+#pragma unroll
+            for (int i = 0; i < KL; i++) {
+                const int k = r + 16 * i;
+                if (k < K && k >= wlo && k < wlo + ww)
+                    wcp[k] = wv[i];
+            }
+    }
+    if (pk3)
+#pragma unroll
+        for (int i = 0; i < KL; i++) {
+            const int k = r + 16 * i;
+            if (k < K && k >= b - 1 && k <= b + 1)
+                pk3[(size_t)(fr * P + p) * 3 + 1 - b + k] = sv[i];
+        }
+    } else
+#endif
+    {
 #pragma unroll
     for (int i = 0; i < KL; i++) {
         const int k = r + 16 * i;
@@ -923,6 +967,7 @@ __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa
             if (pk3 && k >= b - 1 && k <= b + 1)
                 pk3[(size_t)(fr * P + p) * 3 + 1 - b + k] = sv[i];
         }
+    }
     }
     if (r == 0) {
         out.lags[fr * P + p] = b - S;
@@ -1268,10 +1313,11 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (!F16_NO_OUT && mine && 4 * wv < P && pe < P) {
             const int r = t & 15, lo = (int)(e16_rng & 0xFFu), wd = (int)((e16_rng >> 8) & 0xFFu),
                       of = (int)(e16_rng >> 16);
+            constexpr bool SPL = F16_OUT16_LOOPS != 0;
             if (kp.K <= 96)
-                frame16_out16<6>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
+                frame16_out16<6, SPL>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
             else
-                frame16_out16<8>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
+                frame16_out16<8, SPL>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
         }
     };
     auto gate_of = [&](int64_t f) {
