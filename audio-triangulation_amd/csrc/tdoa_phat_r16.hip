@@ -132,8 +132,10 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 // step, config 3 3.57 vs 3.42 -- the pass-2 interval feeds pass 3's VALU-bound DFT)
 #ifndef F16_OUT16_LOOPS
 // frame16_out16: a loop per output kind under its pointer test (0: one loop
-// with the tests inside; config 3 1.925e7 -> 1.967e7, config 4 equal)
-#define F16_OUT16_LOOPS 1
+// with the tests inside; 1: config 3 1.925e7 -> 1.967e7, config 4 equal; 2:
+// as 1, and with the compact scratch the only weighted output each lag's prior
+// read next to its store: config 3 1.966e7 -> 1.980e7, config 4 equal)
+#define F16_OUT16_LOOPS 2
 #endif
 #ifndef F16_EPI_SPLIT
 #define F16_EPI_SPLIT 0
@@ -922,7 +924,11 @@ __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa
         for (int i = 0; i < KL; i++)
             if (r + 16 * i < K)
                 out.scores_f[gb + r + 16 * i] = sv[i];
+#if F16_OUT16_LOOPS == 2
+    if (out.weighted_f) {
+#else
     if (out.weighted_f || wcp) {
+#endif
         float wv[KL];
 #pragma unroll
         for (int i = 0; i < KL; i++) {
@@ -942,6 +948,18 @@ __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa
                     wcp[k] = wv[i];
             }
     }
+#if F16_OUT16_LOOPS == 2
+    else if (wcp) {
+        // the compact scratch alone (the bench path): each lag's prior read next
+        // to its store, as in the one-loop form
+#pragma unroll
+        for (int i = 0; i < KL; i++) {
+            const int k = r + 16 * i;
+            if (k < K && k >= wlo && k < wlo + ww)
+                wcp[k] = sv[i] * priorl[k > b ? k - b : b - k];
+        }
+    }
+#endif
     if (pk3)
 #pragma unroll
         for (int i = 0; i < KL; i++) {
@@ -1306,7 +1324,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // the waves (four pairs each) whose outputs run after the forward's pass-2
     // stores; the rest after its pass-3 stores (F16_EPI_SPLIT: -1 half, else count)
     constexpr int EPW = (P + 3) / 4, EPS = F16_EPI_SPLIT < 0 ? EPW / 2 : (F16_EPI_SPLIT < EPW ? F16_EPI_SPLIT : EPW);
-    auto epi16 = [&](int64_t f, int ps) {
+    auto epi16 = [&](int64_t f, int ps) __attribute__((always_inline)) {
         const int t = opaque_idx((int)threadIdx.x);
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = t >> 4;
         const bool mine = ps == 0 || (ps == 2 ? wv < EPS : wv >= EPS);
@@ -1320,7 +1338,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 frame16_out16<8, SPL>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
         }
     };
-    auto gate_of = [&](int64_t f) {
+    auto gate_of = [&](int64_t f) __attribute__((always_inline)) {
         if (threadIdx.x == 0 && out.gate) {
             int tot = 0;
             for (int q = 0; q < P; q++)
@@ -1408,7 +1426,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             F16_MARK();  // the forward's barriers (diagnostic build)
     };
     if constexpr (ELAG) {
-        auto lag_hook = [&](int ps) {
+        auto lag_hook = [&](int ps) __attribute__((always_inline)) {
             if (prev >= 0)
                 epi16(prev, ps);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
         };

@@ -1,5 +1,5 @@
 set -o pipefail
-export TAG=s1
+export TAG=f3
 mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test:tests/test_gpu_stream.py,tests/test_gpu_parity.py,tests/test_gpu_variants.py && \
-STEPS=400 BENCH_ARGS="--config 5 --engine direct" tools/gpu/run.sh ablib:libtdoa_e0,libtdoa_eA,libtdoa,libtdoa_e0,libtdoa_eA,libtdoa,libtdoa_e0,libtdoa_eA,libtdoa
+tools/gpu/run.sh test smoke && \
+tools/gpu/run.sh bench:3 bench:4 kstats:3 kstats:4
