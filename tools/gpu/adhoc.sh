@@ -1,5 +1,5 @@
 set -o pipefail
-export TAG=f3
+export TAG=n1
 mkdir -p gpurun_out/$TAG
-tools/gpu/run.sh test smoke && \
-tools/gpu/run.sh bench:3 bench:4 kstats:3 kstats:4
+STEPS=8 BENCH_ARGS="--config 4" tools/gpu/run.sh ablib:libtdoa_nolag,libtdoa,libtdoa_nolag,libtdoa && \
+STEPS=60 BENCH_ARGS="--config 3" tools/gpu/run.sh ablib:libtdoa_nolag,libtdoa,libtdoa_nolag,libtdoa
