@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "tdoa_localize_batch", "tdoa_correlate_prepared", "tdoa_average_batch",
     "tdoa_decay_us", "tdoa_get_window", "tdoa_get_mics", "tdoa_get_lut",
     "tdoa_get_prior", "tdoa_dpss_q15", "tdoa_last_error", "tdoa_abi_version", "tdoa_batch_kernel",
-    "tdoa_batch_grid_fused",
+    "tdoa_batch_grid_fused", "tdoa_gpu_clock_mhz",
     "tdoa_heatmap", "tdoa_stream_create", "tdoa_stream_step", "tdoa_stream_reset", "tdoa_stream_state",
     "tdoa_stream_destroy",
     # tdoa_reference_abi.h
@@ -128,6 +128,7 @@ def load() -> C.CDLL:
     L.tdoa_batch_kernel.restype = C.c_char_p
     L.tdoa_batch_grid_fused.argtypes = [P]
     L.tdoa_batch_grid_fused.restype = C.c_int
+    L.tdoa_gpu_clock_mhz.argtypes = [C.c_int, P, C.c_double, C.POINTER(C.c_double)]
     L.tdoa_heatmap.argtypes = [P, P, P, C.c_int, I64, P, P]
     L.tdoa_stream_create.argtypes = [P, I32, I32, P, I64, C.c_int, C.POINTER(P)]
     L.tdoa_stream_step.argtypes = [P, C.POINTER(StreamOutputs), P]

@@ -93,6 +93,19 @@ def dominant_kernel(config: int, engine: str, first: str = "", fused: bool = Tru
     return ""
 
 
+def gpu_clock_mhz(dev, stream):
+    """The shader clock the box holds under VALU load, probed right after the
+    timed region (tdoa_gpu_clock_mhz: every CU's waves run FMA chains for 2 ms
+    and compare s_memtime with the 100 MHz s_memrealtime; median over waves).
+    Boxes of the pool differ by several percent on the same build: this tells
+    a slow box from a regression.  None if the probe fails."""
+    import ctypes as C
+    import tdoa
+    mhz = C.c_double(0.0)
+    rc = tdoa.load().tdoa_gpu_clock_mhz(int(dev.index), C.c_void_p(stream.cuda_stream), 2.0, C.byref(mhz))
+    return round(mhz.value, 1) if rc == 0 else None
+
+
 def phat_flops(M, N):
     """SURVEY.md 8(d) GCC-PHAT flop model per localization, L = 2N."""
     import math
@@ -257,6 +270,7 @@ def time_engine(engine, args, dev, ri, cache):
                     args.warmup, sync=lambda: torch.cuda.synchronize(dev), device=dev,
                     on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # GPU time per launch, launch stream
+    clock = gpu_clock_mhz(dev, stream)
     total = shard.sum_over_ranks([B * args.steps], device=dev)[0]
     # algorithmic bytes: frames in, lags + (x, y) out (+ xy_ls and its rms with LS)
     bytes_per_loc = M * N * 2 + 4 * P + 8 + (12 if ls else 0)
@@ -274,6 +288,7 @@ def time_engine(engine, args, dev, ri, cache):
         "rotate_batches": R,
         "preflight_steps": pre_n,
         "ls": ls,
+        "gpu_clock_mhz": clock,
     }
     lags = out["lags"].cpu()
     assert int(lags.abs().max()) <= loc.dims.S
@@ -312,6 +327,7 @@ def time_stream(args, dev, ri, cache):
                     sync=lambda: (st.synchronize(), torch.cuda.synchronize(dev)), device=dev,
                     on_start=lambda: ev0.record(st), on_end=lambda: ev1.record(st))
     gpu_s = ev0.elapsed_time(ev1) / 1e3
+    clock = gpu_clock_mhz(dev, st)
     _, trig1, gated1 = pipe.totals()
     trig, gated = shard.sum_over_ranks([trig1 - trig0, gated1 - gated0], device=dev)
     # per-hop latency, outside the timed region: one hop in flight at a time,
@@ -335,6 +351,7 @@ def time_stream(args, dev, ri, cache):
     return {"engine": "direct", "value": trig / t["wall_max_s"],
             "ms_per_step": t["wall_max_s"] * 1e3 / args.steps,
             "kernel_ms": gpu_s * 1e3 / args.steps, "triggered": trig, "gated": gated,
+            "gpu_clock_mhz": clock,
             "stream_samples_per_s": samples / t["wall_max_s"],
             "realtime_streams": samples / t["wall_max_s"] / cfg["fs"],
             "capture_bytes_per_step": ri.world * S * H * 3,
@@ -725,6 +742,7 @@ def main():
                           "note": "untimed, before the warmups: every rotating batch once, then "
                                   "steps until the time has passed"},
             "ms_per_step": main_res["ms_per_step"],
+            "gpu_clock_mhz": main_res["gpu_clock_mhz"],
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,
@@ -791,6 +809,7 @@ def main_stream(args, dev, ri, cache):
             "value": res["value"], "unit": "localizations/s", "n_gpus": world,
             "ranks_seen": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+            "gpu_clock_mhz": res["gpu_clock_mhz"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int16->int64",
             "data": "synthetic u8 capture bytes (bursts from a fixed source per stream over a "
@@ -812,7 +831,21 @@ def main_stream(args, dev, ri, cache):
                          / HBM_PEAK_GBS,
                          **dict(zip(("traffic", "traffic_source"), stream_traffic(args))),
                          "kernel": "all kernels of a hop (hipGraph)", "kernel_ms": res["kernel_ms"],
-                         "bytes_per_step": res["capture_bytes_per_step"] // ri.world},
+                         "bytes_per_step": res["capture_bytes_per_step"] // ri.world,
+                         # what the sliding trigger must read per hop: the half-window
+                         # sums after every sample need the entering sample (this hop),
+                         # the one crossing the window's middle (N/2 = one hop back) and
+                         # the leaving one (N = two hops back): 3 x the hop's capture
+                         # bytes (rolling_buffer.c:16-41 per sample, sample_compute.h:75-91)
+                         "sliding": {
+                             "bytes_per_step": 3 * res["capture_bytes_per_step"] // ri.world,
+                             "achieved": 3 * res["capture_bytes_per_step"] / ri.world /
+                             (res["kernel_ms"] * 1e-3) / 1e9,
+                             "frac": 3 * res["capture_bytes_per_step"] / ri.world /
+                             (res["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "note": "the trigger's algorithmic reads (current hop + the two hops "
+                                     "leaving the half-windows); `traffic` counts these plus the "
+                                     "triggered frames DIRECT reads and the EMA states"}},
             "cpu_baseline": None,
         }
         if not args.no_cpu:  # rank 0, after the timed region, at every world size

@@ -219,6 +219,12 @@ const char *tdoa_batch_kernel(const tdoa_ctx *ctx);
  * inside that first kernel (no weighted-score scratch, no separate grid
  * launch), 0 if a grid kernel follows it (diagnostics, like tdoa_batch_kernel). */
 int tdoa_batch_grid_fused(const tdoa_ctx *ctx);
+/* Measurement: the shader clock (MHz) `device` holds under VALU load -- every
+ * CU's waves run FMA chains for about `ms` milliseconds (0 < ms <= 100) on
+ * `stream` and compare s_memtime with the 100 MHz s_memrealtime; the median
+ * over waves.  Synchronous.  bench.py records it after its timed region so a
+ * slow box and a regression can be told apart. */
+int tdoa_gpu_clock_mhz(int device, void *stream, double ms, double *mhz);
 
 #ifdef __cplusplus
 }
