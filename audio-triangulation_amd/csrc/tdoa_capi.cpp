@@ -328,6 +328,13 @@ uint16_t bb_query(int P, int K, int p, int lo, int hi)
     const int n = hi - lo + 1;
     if (n > 15)
         return 0x1FFF;  // wide: the table is not used (kp.bb_wide)
+    // The query's two windows [lo, lo + 2^lv) and [hi + 1 - 2^lv, hi + 1) lie
+    // inside [lo, hi] (2^lv <= n), and k_grid_bb's level build reads lags past
+    // K - 1 (unclamped 16-B reads, tdoa_grid_bb.h): those level elements are
+    // never queried only while every range stays inside the lag range.  A
+    // range that does not is encoded wide (the exhaustive k_grid runs instead).
+    if (lo < 0 || hi >= K || n < 1)
+        return 0x1FFF;
     const int lv = n >= 8 ? 3 : (n >= 4 ? 2 : (n >= 2 ? 1 : 0));
     const int KS = P > 8 ? (K + 3) & ~3 : K;  // bb_ks (tdoa_grid_bb.h): score row stride
     const int PKp = (P * KS + 3) & ~3, RW = K <= 96 ? 96 : 128;
@@ -684,6 +691,8 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             kp.p1k_img = c->d_p1k_img;
             kp.p1k_img_bytes = (int32_t)img.size();
         }
+#if TDOA_AB
+        // the one-frame-per-wave A/B kernel's image (tdoa/libtdoa_ab.so only)
         tdoa_p1k_w64_image(M, N, c->K, c->U, c->win.data(), c->prior.data(), c->tuples.data(), img);
         if (!img.empty()) {
             if (hipMalloc(&c->d_w64_img, img.size()) != hipSuccess ||
@@ -695,6 +704,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             kp.w64_img = c->d_w64_img;
             kp.w64_img_bytes = (int32_t)img.size();
         }
+#endif
         if (tdoa_gcc_phat_needs_split(M, N)) {
             const size_t want = (size_t)128 << 20;
             if (hipMalloc(&c->d_spec, want) != hipSuccess) {
@@ -768,7 +778,10 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
             kp.wc_CK = off;
             kp.wc_nch = (int32_t)c->wc_chunks.size();
             kp.wc_chunks = (const uint32_t *)c->d_wc;
-            // the fused k_frame16 grid's queries (tdoa_internal.h, kp.fg_q)
+#if TDOA_AB
+            // the fused k_frame16 grid's queries (tdoa_internal.h, kp.fg_q): an
+            // A/B path, built only into tdoa/libtdoa_ab.so (every
+            // context paid O(U P) host work and a device table for it)
             std::vector<uint16_t> fq((size_t)kp.bb_NT * 32, 0);
             bool fok = off <= 2048 && kp.bb_NT <= 256 && c->P <= 32;
             for (int t = 0; fok && t < kp.bb_NT; t++)
@@ -808,6 +821,7 @@ extern "C" int tdoa_create(const tdoa_config *cfg, int device, tdoa_ctx **out)
                 kp.fg_tup = (const uint16_t *)((const char *)c->d_fgq + qbytes);
                 kp.fg_ok = 1;
             }
+#endif
         }
     }
     *out = c;

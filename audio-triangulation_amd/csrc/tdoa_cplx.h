@@ -129,7 +129,10 @@ __device__ __forceinline__ f2 c_unit(f2 x, float e2)
     f2 rr;
     rr.x = __builtin_amdgcn_rsqf(m);
     f2 y;
-    asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(rr));
+#ifndef TDOA_UNIT_NOP
+#define TDOA_UNIT_NOP "s_nop 0\n\t"  // the trans-use wait state (tools/co_audit.py checks it)
+#endif
+    asm(TDOA_UNIT_NOP "v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(y) : "v"(x), "v"(rr));
     return y;
 #else
     const float r = __builtin_amdgcn_rsqf(__builtin_fmaf(x.x, x.x, __builtin_fmaf(x.y, x.y, e2)));

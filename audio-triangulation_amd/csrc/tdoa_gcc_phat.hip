@@ -9,6 +9,10 @@
 #ifndef TDOA_P1K_DEFAULT_W64
 #define TDOA_P1K_DEFAULT_W64 0
 #endif
+// TDOA_AB=1: the A/B build (tdoa/libtdoa_ab.so) with k_p1k_w64 behind TDOA_P1K=w64
+#ifndef TDOA_AB
+#define TDOA_AB 0
+#endif
 #include <stdint.h>
 
 #include <climits>
@@ -281,6 +285,11 @@ int hip_fail(hipError_t e, const char *what)
 //     the second DFT-32 evaluates just its outputs 0 and 31 per lane;
 //   * 2 frames per 192-thread workgroup (6 half-waves = 6 FFTs), persistent
 //     over frame pairs with the next pair's samples prefetched in registers.
+// Since round 2 it is the fallback of the config-2 shape (tuple tables larger
+// than k_p1k_lean's LDS image holds).  One workgroup per CU (launch bounds
+// 192, 1): at two it spilled 7 VGPRs to 32 B of scratch; with the unified
+// register file of a one-wave-per-SIMD launch it holds 258 registers and no
+// scratch (tools/co_audit.py, tests/test_code_objects.py).
 
 #ifdef TDOA_DIAG
 // diagnostic build only: per-workgroup cycles per phase of k_gcc_phat_1024
@@ -386,7 +395,7 @@ __device__ __forceinline__ void grid_tail(const tdoa_kparams &kp, const tdoa_kou
     }
 }
 
-__global__ void __launch_bounds__(192, 2) k_gcc_phat_1024(tdoa_kparams kp, tdoa_kout out,
+__global__ void __launch_bounds__(192, 1) k_gcc_phat_1024(tdoa_kparams kp, tdoa_kout out,
                                                           const int16_t *__restrict__ frames,
                                                           int64_t B, float eps2)
 {
@@ -671,19 +680,26 @@ bool tdoa_phat1024_fits(const tdoa_kparams &kp);
 int tdoa_launch_phat1024(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames,
                          int64_t B, float phat_eps, void *stream);
 
-// one frame per 64-lane wave (tdoa_p1k_w64.hip)
+#if TDOA_AB
+// one frame per 64-lane wave (tdoa_p1k_w64.hip, A/B build only)
 bool tdoa_p1k_w64_fits(const tdoa_kparams &kp);
 int tdoa_launch_p1k_w64(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *frames, int64_t B,
                         float phat_eps, void *stream);
-// config-2 kernel choice: TDOA_P1K=lean | w64 (A/B runs), else the default
+#endif
+// config-2 kernel choice: TDOA_P1K=lean | w64 (A/B runs, A/B build), else the default
 static bool use_w64(const tdoa_kparams &kp)
 {
+#if !TDOA_AB
+    (void)kp;
+    return false;
+#else
     static const int pick = [] {
         const char *e = getenv("TDOA_P1K");
         return e && !strcmp(e, "w64") ? 1 : (e && !strcmp(e, "lean") ? 0 : -1);
     }();
     const bool want = pick < 0 ? TDOA_P1K_DEFAULT_W64 : pick == 1;
     return want && tdoa_p1k_w64_fits(kp);
+#endif
 }
 
 bool tdoa_phat_r16_fits(int M, int N, int S);
@@ -768,8 +784,10 @@ int tdoa_launch_gcc_phat(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (!kp.tw || !kp.tw2)
         return tdoa_set_error(-1, "GCC_PHAT: context has no twiddle tables");
     const PhatRoute route = phat_route(kp);
+#if TDOA_AB
     if (route == PhatRoute::W64)
         return tdoa_launch_p1k_w64(kp, out, frames, B, phat_eps, stream);
+#endif
     if (route == PhatRoute::P1K_LEAN)
         return tdoa_launch_phat1024(kp, out, frames, B, phat_eps, stream);
     if (route == PhatRoute::R16)

@@ -123,6 +123,16 @@ bool have_avx2()
     return yes;
 }
 
+// vpmaddwd's pair sum wraps only for (-32768)^2 + (-32768)^2: `a` without an
+// INT16_MIN keeps every lane below 2^31
+bool has_int16_min(const int16_t *a)
+{
+    int any = 0;
+    for (int i = 0; i < N; i++)
+        any |= a[i] == INT16_MIN;
+    return any != 0;
+}
+
 }  // namespace
 
 // correlations.c:7-33.  score[s + S] = sum_i a[i + max(0, -s)] * b[i + max(0, s)]
@@ -133,7 +143,7 @@ void correlate(const int16_t *a, const int16_t *b, const float *prior, int64_t *
     alignas(32) int16_t bpad[S + N + S + 16];
     std::memset(bpad, 0, sizeof bpad);
     std::memcpy(bpad + S, b, sizeof(int16_t) * N);
-    if (have_avx2())
+    if (have_avx2() && !has_int16_min(a))
         scores_avx2(a, bpad, corr);
     else
         scores_scalar(a, bpad, corr);

@@ -156,6 +156,28 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_XS
 #define F16_XS 1
 #endif
+// the lagged epilogue's lambdas forced inline (F16_LAMBDA_AI=0: the inliner
+// decides -- an A/B build for the ISA audit only, see DESIGN.md "k_frame16:
+// the two unexplained failures")
+// TDOA_AB=1: the A/B build (Makefile "ab", tdoa/libtdoa_ab.so for tools and the
+// variant tests): k_frame16w and the fused grid (FG) are compiled in; the
+// product library holds only the dispatched kernels
+#ifndef TDOA_AB
+#define TDOA_AB 0
+#endif
+// the four-pairs epilogue's compact ranges as the wave's four scalar loads
+// and a per-lane pick (F16_RNG_SCALAR=1: A/B build for the ISA audit only)
+#ifndef F16_RNG_SCALAR
+#define F16_RNG_SCALAR 0
+#endif
+#ifndef F16_LAMBDA_AI
+#define F16_LAMBDA_AI 1
+#endif
+#if F16_LAMBDA_AI
+#define F16_AI __attribute__((always_inline))
+#else
+#define F16_AI
+#endif
 __host__ __device__ constexpr int xs(int i) { return i ^ ((i >> 4) & 15); }
 template <bool XS>
 __host__ __device__ constexpr int lidx(int i) { return XS ? xs(i) : pidx(i); }
@@ -988,7 +1010,9 @@ __device__ __forceinline__ void frame16_out16(const tdoa_kparams &kp, const tdoa
     }
     }
     if (r == 0) {
+#ifndef F16_RNG_DUMP  // (the dump build owns out.lags, see the frame loop's end)
         out.lags[fr * P + p] = b - S;
+#endif
         lagl[p] = b - S;
     }
 }
@@ -1311,11 +1335,41 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     if constexpr (OUT16) {
         const int e16_p = (int)threadIdx.x >> 4;  // wave w, row q: pair 4 w + q
         const int pq = e16_p < P ? e16_p : 0;
-        // per-lane loads, waited for below (selecting each row's range from four
-        // scalar loads gave wrong compact offsets for some pairs with this
-        // compiler: bench-path test cfg4, cells 72 % equal; not understood)
+        // per-lane loads, waited for below.  Workaround for a codegen bug: picking
+        // each row's range from the wave's four scalar loads (F16_RNG_SCALAR=1)
+        // makes hipcc address wc_off[p] (u16, p = 4 w + 2) as SBASE = kernarg + p,
+        // SOFFSET = p, and gfx950's scalar loads drop the base's low two address
+        // bits: every wave's row 2 read the offset of its row 0 (round 5: cfg4
+        // cells 72 % equal; root cause round 6, tools/probe/smem_sbase_align.hip,
+        // tools/diag_rng.py; tests/test_code_objects.py flags the pattern)
+#if F16_RNG_SCALAR
+        // A/B for the ISA audit: the wave's four ranges as scalar loads, the
+        // row's picked by a per-lane select
+        (void)pq;
+        const int w0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        uint32_t rq[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int p = 4 * w0 + q < P ? 4 * w0 + q : 0;
+            rq[q] = (uint32_t)kp.wc_lo[p] | (uint32_t)kp.wc_w[p] << 8 | (uint32_t)kp.wc_off[p] << 16;
+        }
+        const int row = ((int)threadIdx.x >> 4) & 3;
+#if F16_RNG_SCALAR == 2
+        // branch-free: the four ranges forced into SGPRs, a v_cndmask chain
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            rq[q] = __builtin_amdgcn_readfirstlane(rq[q]);
+        e16_rng = rq[0];
+        e16_rng = row == 1 ? rq[1] : e16_rng;
+        e16_rng = row == 2 ? rq[2] : e16_rng;
+        e16_rng = row == 3 ? rq[3] : e16_rng;
+#else
+        e16_rng = row == 0 ? rq[0] : (row == 1 ? rq[1] : (row == 2 ? rq[2] : rq[3]));
+#endif
+#else
         const auto *kk = kernarg_kp();
         e16_rng = (uint32_t)kk->wc_lo[pq] | (uint32_t)kk->wc_w[pq] << 8 | (uint32_t)kk->wc_off[pq] << 16;
+#endif
         asm volatile("" : "+v"(e16_rng));
     }
     // DM 1 (four-pairs epilogue), lagged (F16_EPI_LAG): frame f's outputs run in
@@ -1324,7 +1378,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // the waves (four pairs each) whose outputs run after the forward's pass-2
     // stores; the rest after its pass-3 stores (F16_EPI_SPLIT: -1 half, else count)
     constexpr int EPW = (P + 3) / 4, EPS = F16_EPI_SPLIT < 0 ? EPW / 2 : (F16_EPI_SPLIT < EPW ? F16_EPI_SPLIT : EPW);
-    auto epi16 = [&](int64_t f, int ps) __attribute__((always_inline)) {
+    auto epi16 = [&](int64_t f, int ps) F16_AI {
         const int t = opaque_idx((int)threadIdx.x);
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = t >> 4;
         const bool mine = ps == 0 || (ps == 2 ? wv < EPS : wv >= EPS);
@@ -1338,7 +1392,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 frame16_out16<8, SPL>(kp, out, scl, priorl, lagl, f, P, pe, r, lo, wd, of);
         }
     };
-    auto gate_of = [&](int64_t f) __attribute__((always_inline)) {
+    auto gate_of = [&](int64_t f) F16_AI {
         if (threadIdx.x == 0 && out.gate) {
             int tot = 0;
             for (int q = 0; q < P; q++)
@@ -1426,7 +1480,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             F16_MARK();  // the forward's barriers (diagnostic build)
     };
     if constexpr (ELAG) {
-        auto lag_hook = [&](int ps) __attribute__((always_inline)) {
+        auto lag_hook = [&](int ps) F16_AI {
             if (prev >= 0)
                 epi16(prev, ps);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
         };
@@ -1741,6 +1795,13 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             __syncthreads();
             gate_of(prev);
         }
+#ifdef F16_RNG_DUMP
+        // diagnostic builds only: every thread's packed compact range over the
+        // first 1024 lag slots (tools/diag_rng.py)
+        __syncthreads();
+        if (blockIdx.x == 0)
+            out.lags[threadIdx.x] = (int32_t)e16_rng;
+#endif
     }
     if constexpr (FG) {
         // the last frame's grid, by waves 0 .. FG_NGW - 1 (every buffer is free)
@@ -1835,6 +1896,9 @@ static bool frame16_defer(const tdoa_kparams &kp)
 template <int C, int M>
 static bool frame16_fg(const tdoa_kparams &kp)
 {
+#if !TDOA_AB
+    return false;  // the fused grid is an A/B path (tools libraries only)
+#endif
     if (!fg_shape<C, M>() || !kp.fg_ok || !kp.fg_q || !kp.fg_tup || fg_mode() == 0 || kp.P != M * (M - 1) / 2)
         return false;
     const bool defer = frame16_defer<C, M>(kp);
@@ -1855,11 +1919,15 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
     // the grid solved in the kernel when the caller asks for it (FG)
     const bool fg = frame16_fg<C, M>(kp) && (out.cell || out.xy || out.max_Lf);
     const void *fn;
+#if TDOA_AB
     if constexpr (fg_shape<C, M>())
         fn = defer ? (fg ? (const void *)k_frame16<C, M, 1, F16_XS != 0, true> : (const void *)k_frame16<C, M, 1>)
                    : (fg ? (const void *)k_frame16<C, M, 0, F16_XS != 0, true> : (const void *)k_frame16<C, M, 0>);
     else
         fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
+#else
+    fn = defer ? (const void *)k_frame16<C, M, 1> : (const void *)k_frame16<C, M, 0>;
+#endif
     const size_t lds =
         (defer ? frame16_lds_base<C>() + (size_t)P * kp.K * sizeof(float) : frame16_lds_base<C>()) +
         (fg ? fg_lds_bytes(kp, defer) : 0);
@@ -1870,6 +1938,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
     if (res < 1)
         return tdoa_set_error(-2, "k_frame16: no resident workgroup (LDS / registers)");
     const int64_t grid = B < (int64_t)res ? B : (int64_t)res;
+#if TDOA_AB
     if constexpr (fg_shape<C, M>()) {
         if (fg) {
             if (defer)
@@ -1880,6 +1949,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
                                    kpl, out, frames, B, e2);
         }
     }
+#endif
     if (!fg) {
         if (defer)
             hipLaunchKernelGGL((k_frame16<C, M, 1>), dim3((unsigned)grid), dim3(1024), lds, st, kp, out, frames, B, e2);
@@ -1896,6 +1966,7 @@ int launch_frame16(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t *
 }
 
 
+#if TDOA_AB  // the A/B kernel k_frame16w: built into tools libraries only (Makefile "ab")
 // ------------------------------------------------ fused, one wave per pair
 // k_frame16w<2048, 8> (BASELINE config 4).  k_frame16's forward transforms,
 // then the split writes the unit spectra U_m[0..C] back into the mics' LDS
@@ -2283,12 +2354,16 @@ int launch_frame16w(const tdoa_kparams &kp, const tdoa_kout &out, const int16_t 
     }
     return 0;
 }
+#endif  // TDOA_AB
 
 // k_frame16w (one wave per pair) or k_frame16 (a group of waves per pair) for
 // config 4's shape: TDOA_F16=w | grp, default grp (measured: 106.2 vs 103.2
 // ms per config-4 step, both with volatile LDS reads)
 bool frame16w_pick()
 {
+#if !TDOA_AB
+    return false;  // the product library has only k_frame16
+#endif
     static const int pick = [] {
         const char *e = getenv("TDOA_F16");
         return e && !strcmp(e, "w") ? 1 : 0;
@@ -2406,8 +2481,11 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
     if (kp.N == 4096 && kp.M == 3)
         return launch_frame16<4096, 3>(kp, out, frames, B, e2, st);
     if (kp.N == 2048 && kp.M == 8)
-        return frame16w_pick() ? launch_frame16w<2048, 8>(kp, out, frames, B, e2, st)
-                               : launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
+#if TDOA_AB
+        if (frame16w_pick())
+            return launch_frame16w<2048, 8>(kp, out, frames, B, e2, st);
+#endif
+        return launch_frame16<2048, 8>(kp, out, frames, B, e2, st);
     if (kp.N == 2048 && kp.M == 4)
         return launch_frame16<2048, 4>(kp, out, frames, B, e2, st);
     return kp.N == 4096 ? launch_r16<4096>(kp, out, frames, B, e2, scratch, scratch_bytes, st)

@@ -16,7 +16,9 @@ Every case also checks the cell / max_Lf bit for bit against the exhaustive
 float32 scan of the run's own weighted scores (vga_heatmap.h:99-108).
 
 The defaults (k_frame16, deferred lagged epilogue at configs 3 and 4) run in
-test_gpu_gcc_phat.py itself.
+test_gpu_gcc_phat.py itself.  k_frame16w and the fused grid are A/B paths that
+measured slower: they are built only into tdoa/libtdoa_ab.so (Makefile "ab",
+TDOA_AB=1), which those children load through TDOA_LIB; libtdoa.so has neither.
 """
 import os
 import subprocess
@@ -27,6 +29,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+AB_LIB = os.path.join(ROOT, "audio-triangulation_amd", "tdoa", "libtdoa_ab.so")
 
 CHILD = r"""
 import sys
@@ -53,7 +56,7 @@ assert (got["cell"] == cell).all() and (got["max_Lf"] == mx).all()
 lean = _np(ph.localize(fr))  # no scores requested: the bench's path
 for k in lean:
     assert np.array_equal(lean[k], got[k]), k
-print("variant ok", ph.batch_kernel())
+print("variant ok", ph.batch_kernel(), "grid_fused", ph.batch_grid_fused())
 """
 
 
@@ -70,6 +73,12 @@ def test_frame16_variant_vs_fp64(env, M, N):
     code = CHILD.format(pkg=os.path.join(ROOT, "audio-triangulation_amd"), orc=os.path.join(ROOT, "oracle"),
                         tests=os.path.join(ROOT, "tests"), M=M, N=N)
     e = dict(os.environ, **env)
+    if "TDOA_F16" in env or "TDOA_F16_FG" in env:  # the A/B kernels live in the A/B library
+        e["TDOA_LIB"] = AB_LIB
     r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "variant ok" in r.stdout
+    if env.get("TDOA_F16") == "w":
+        assert "variant ok k_frame16w" in r.stdout, r.stdout
+    if env.get("TDOA_F16_FG") == "1":
+        assert "grid_fused True" in r.stdout, r.stdout

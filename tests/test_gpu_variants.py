@@ -12,7 +12,9 @@ switches once per process -- against the same oracles as the defaults:
                      sample_compute.h:53-146 (test_gpu_stream.py's compare)
 
 The frame16 switches are tests/test_gpu_frame16_variants.py; TDOA_NO_COMPACT
-is tests/test_gpu_bench_path.py.
+is tests/test_gpu_bench_path.py.  k_p1k_w64 measured slower and is built only
+into the A/B library tdoa/libtdoa_ab.so (Makefile "ab"), loaded here through
+TDOA_LIB; libtdoa.so does not contain it.
 """
 import os
 import subprocess
@@ -23,6 +25,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+AB_LIB = os.path.join(ROOT, "audio-triangulation_amd", "tdoa", "libtdoa_ab.so")
 PATHS = [os.path.join(ROOT, "audio-triangulation_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
 
 W64 = r"""
@@ -87,7 +90,7 @@ def _child(code, env):
 
 
 def test_p1k_w64_vs_fp64_and_exhaustive_grid():
-    _child(W64.format(golden=os.path.join(ROOT, "tests", "golden", "pipeline_cfg2.npz")), {"TDOA_P1K": "w64"})
+    _child(W64.format(golden=os.path.join(ROOT, "tests", "golden", "pipeline_cfg2.npz")), {"TDOA_P1K": "w64", "TDOA_LIB": AB_LIB})
 
 
 def test_ema_waves_12_stream_bit_exact():

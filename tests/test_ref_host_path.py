@@ -122,3 +122,36 @@ def test_gpu_device_switch_rules():
     assert L.tdoa_ref_set_device(-1) == 0
     assert L.tdoa_ref_set_device(-7) == 0  # any negative: the host path
     assert L.tdoa_ref_set_device(0) == 0
+
+
+@pytest.mark.parametrize("case", ["runs", "all_min", "alternating", "random_with_min"])
+def test_correlations_init_int16_min(host_lib, oracle, case):
+    """correlations_init takes any buffer_t, not only windowed ones:
+    adjacent INT16_MIN samples in both buffers make a vpmaddwd pair sum
+    (-32768)^2 * 2 = 2^31, which wraps in an int32 lane; the reference
+    multiplies in int32 and sums in int64 (correlations.c:9-18).  Bit-exact
+    against the oracle for raw buffers with runs of -32768."""
+    L = host_lib
+    rng = np.random.default_rng(0x3276)
+    n = 1024
+    if case == "runs":
+        a = rng.integers(-32768, 32768, n).astype(np.int16)
+        b = rng.integers(-32768, 32768, n).astype(np.int16)
+        for lo in (0, 100, 511, 1000):
+            a[lo:lo + 24] = -32768
+            b[lo + 3:lo + 30] = -32768
+    elif case == "all_min":
+        a = np.full(n, -32768, np.int16)
+        b = np.full(n, -32768, np.int16)
+    elif case == "alternating":
+        a = np.where(np.arange(n) % 4 < 2, -32768, 32767).astype(np.int16)
+        b = a.copy()
+    else:
+        a = rng.choice(np.array([-32768, -32767, 0, 32767], np.int16), n)
+        b = rng.choice(np.array([-32768, 32767], np.int16), n)
+    for x, y in ((a, b), (b, a), (a, a)):
+        corr = _lib.Correlations()
+        L.correlations_init(C.byref(corr), C.byref(_buf(x)), C.byref(_buf(y)))
+        sc, best = oracle.xcorr(x, y, 46)
+        assert corr.best_shift == best, case
+        assert (np.frombuffer(bytes(corr.correlations), np.int64) == oracle.prior(sc, best)).all(), case
