@@ -15,7 +15,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# TDOA_ORACLE_LIB: another build of the same restatement (the sanitizer build,
+# tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("TDOA_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libref_components.so")
 
 _lib = None

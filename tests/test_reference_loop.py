@@ -52,16 +52,23 @@ def _i64(a):
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF, "sample_compute.h")),
                     reason="reference sources not present (GPU box)")
 def test_unchanged_reference_loop_runs_on_libtdoa(tmp_path, oracle):
-    lib = os.path.join(PKG, "tdoa", "libtdoa.so")
+    # TDOA_LIB: another build of the library (tests/test_sanitizers.py: the
+    # ASan + UBSan build, whose runtime the process inherits via LD_PRELOAD; the
+    # host program itself stays a gcc build -- the reference's protothread
+    # header uses GCC's labels-as-values in a form clang rejects,
+    # pt_cornell_rp2040_v1_3.h:800,860 -- so only libtdoa's side is instrumented)
+    lib = os.environ.get("TDOA_LIB") or os.path.join(PKG, "tdoa", "libtdoa.so")
     if not os.path.exists(lib):
         pytest.skip("libtdoa.so not built")
     if shutil.which("gcc") is None:
         pytest.skip("no gcc")
     exe = tmp_path / "sample_compute_host"
     cmd = ["gcc", "-std=gnu11", "-O2", "-w", "-I", os.path.join(PKG, "host", "pico_host"),
-           "-I", REF, os.path.join(PKG, "host", "sample_compute_main.c"),
-           "-L", os.path.join(PKG, "tdoa"), "-ltdoa", "-L/opt/rocm/lib", "-lamdhip64", "-lm",
-           "-Wl,--no-undefined", "-Wl,-rpath," + os.path.join(PKG, "tdoa"), "-o", str(exe)]
+           "-I", REF, os.path.join(PKG, "host", "sample_compute_main.c"), lib,
+           "-L/opt/rocm/lib", "-lamdhip64", "-lm",
+           "-Wl,--no-undefined", "-Wl,-rpath," + os.path.dirname(lib), "-o", str(exe)]
+    if os.environ.get("TDOA_SAN") == "1":  # the instrumented library's runtime (clang's, preloaded)
+        cmd[-2:-2] = [os.environ["LD_PRELOAD"]]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     log = tmp_path / "handoffs.bin"
