@@ -913,6 +913,46 @@ static bool env_flag(const char *name)
     return e && *e && strcmp(e, "0") != 0;
 }
 
+// frames per k_frame16 -> k_grid_bb chunk in the compact mode: TDOA_F16_CHUNK
+// (A/B switch; default 0, the whole batch in one launch pair).  Measured at
+// config 4 (same box, ms per 1e6 frames): chunks of 16384 / 32768 frames 87.4 /
+// 86.5 vs 85.8 unchunked -- and the counter traffic does not drop: the compact
+// scores still leave and re-enter the L2 (k_frame16 writes 7.5 GB, k_grid_bb
+// reads 7.1 GB per 1e6 frames, FETCH_SIZE / WRITE_SIZE count L2 <-> fabric
+// requests whether the MALL serves them or HBM does), and each chunk adds two
+// launch tails (DESIGN.md, round-6 negative results)
+static int64_t compact_chunk(int64_t B)
+{
+    static const int64_t chunk = [] {
+        const char *e = getenv("TDOA_F16_CHUNK");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    return chunk > 0 && chunk < B ? chunk : B;
+}
+
+// the outputs of frames [c0, ...) of a batch (per-frame arrays advanced; the
+// compact scratch, reused per chunk, is not)
+static tdoa_kout offset_kout(const tdoa_kout &k, int64_t c0, int P, int K)
+{
+    tdoa_kout o = k;
+    auto adv = [&](auto *&ptr, int64_t per) {
+        if (ptr)
+            ptr += c0 * per;
+    };
+    adv(o.lags, P);
+    adv(o.gate, 1);
+    adv(o.cell, 1);
+    adv(o.xy, 2);
+    adv(o.max_L, 1);
+    adv(o.max_Lf, 1);
+    adv(o.scores, (int64_t)P * K);
+    adv(o.weighted, (int64_t)P * K);
+    adv(o.scores_f, (int64_t)P * K);
+    adv(o.weighted_f, (int64_t)P * K);
+    adv(o.peak3, (int64_t)P * 3);
+    return o;
+}
+
 static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa_outputs *out,
                      void *stream, bool prepared)
 {
@@ -940,8 +980,9 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
     // grid reads, compacted, when k_grid_bb solves the grid (configs 3, 4)
     const bool compact = grid && !weighted && !fused_grid && phat && tdoa_gcc_phat_peak3(ctx->kp) &&
                          tdoa_grid_bb_compact(ctx->kp) && !env_flag("TDOA_NO_COMPACT");
+    const int64_t chunk = compact ? compact_chunk(B) : B;
     if (compact) {
-        int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, (size_t)B * ctx->kp.wc_CK * sizeof(float), stream,
+        int rc = grow(&ctx->d_wscratch, &ctx->wscratch_bytes, (size_t)chunk * ctx->kp.wc_CK * sizeof(float), stream,
                       "weighted-score");
         if (rc)
             return rc;
@@ -985,13 +1026,29 @@ static int run_batch(tdoa_ctx *ctx, const int16_t *frames, int64_t B, const tdoa
             return rc;
         k.cell = (int32_t *)ctx->d_cscratch;
     }
-    int rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, ctx->d_spec,
-                                         ctx->spec_bytes, stream)
+    int rc = 0;
+    if (compact && chunk < B) {
+        // (TDOA_F16_CHUNK, A/B) the compact scratch of one chunk of frames at a
+        // time, reused: k_frame16 writes it and k_grid_bb reads it back while it
+        // can still sit in the 256 MB MALL (16384 x 7.3 KB at config 4)
+        const int64_t M = ctx->kp.M, N = ctx->kp.N;
+        for (int64_t c0 = 0; rc == 0 && c0 < B; c0 += chunk) {
+            const int64_t n = B - c0 < chunk ? B - c0 : chunk;
+            const tdoa_kout kc = offset_kout(k, c0, ctx->P, ctx->K);
+            rc = tdoa_launch_gcc_phat(ctx->kp, kc, frames + c0 * M * N, n, ctx->cfg.phat_eps, ctx->d_spec,
+                                      ctx->spec_bytes, stream);
+            if (rc == 0)
+                rc = tdoa_launch_grid(ctx->kp, kc, weighted, phat, n, stream);
+        }
+    } else {
+        rc = phat ? tdoa_launch_gcc_phat(ctx->kp, k, frames, B, ctx->cfg.phat_eps, ctx->d_spec, ctx->spec_bytes,
+                                         stream)
                   : tdoa_launch_direct(ctx->kp, k, frames, B, prepared, stream, nullptr);
-    if (rc != 0 || !grid)
-        return rc;
-    if (!fused_grid)
-        rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
+        if (rc != 0 || !grid)
+            return rc;
+        if (!fused_grid)
+            rc = tdoa_launch_grid(ctx->kp, k, weighted, phat, B, stream);
+    }
     if (rc != 0 || !ls)
         return rc;
     return tdoa_launch_ls(ctx->kp, raw, phat, k.peak3, k.lags, k.cell, out->xy_ls, out->ls_rms, B, stream);
