@@ -106,6 +106,29 @@ def gpu_clock_mhz(dev, stream):
     return round(mhz.value, 1) if rc == 0 else None
 
 
+def settle(launches, R, dev, stream, max_s):
+    """Untimed windows of launches (max(R, 8) each: every rotating batch) until two
+    consecutive windows' mean launch time (HIP events on the launch stream) agree
+    within 2 %, or max_s has passed.  Returns the windows' means (us) and whether
+    they settled."""
+    n = max(R, 8)
+    means, t0 = [], time.perf_counter()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    while True:
+        e0.record(stream)
+        for k in range(n):
+            launches[k % R]()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        means.append(e0.elapsed_time(e1) * 1e3 / n)
+        ok = len(means) >= 2 and abs(means[-1] - means[-2]) <= 0.02 * means[-2]
+        if ok or time.perf_counter() - t0 > max_s:
+            return {"windows": len(means), "launches_per_window": n, "settled": ok,
+                    "last_window_us": [round(m, 2) for m in means[-3:]],
+                    "first_window_us": round(means[0], 2)}
+
+
 def phat_flops(M, N):
     """SURVEY.md 8(d) GCC-PHAT flop model per localization, L = 2N."""
     import math
@@ -131,6 +154,8 @@ def parse():
                     help="untimed steps for this long before the W warmups (configs 2-4): clocks and "
                          "the rotating batches' translations settle, so a short K-step window "
                          "measures the steady state; 0 disables")
+    ap.add_argument("--settle-max-s", type=float, default=8.0,
+                    help="longest the preflight waits for a steady launch time (configs 2-4)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: rehearse the N-process launch, rank logic and JSON line over gloo "
@@ -264,6 +289,7 @@ def time_engine(engine, args, dev, ri, cache):
         if pre_n % 64 == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
+    steady = settle(launches, R, dev, stream, args.settle_max_s) if args.preflight_s > 0 else None
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t = shard.timed(lambda k: launches[k % R](), args.steps,
@@ -287,6 +313,7 @@ def time_engine(engine, args, dev, ri, cache):
         "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
         "rotate_batches": R,
         "preflight_steps": pre_n,
+        "steady": steady,
         "ls": ls,
         "gpu_clock_mhz": clock,
     }
@@ -739,8 +766,12 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "preflight": {"steps": main_res["preflight_steps"], "seconds": args.preflight_s,
+                          "steady": main_res["steady"],
                           "note": "untimed, before the warmups: every rotating batch once, then "
-                                  "steps until the time has passed"},
+                                  "steps until the time has passed, then windows of launches until "
+                                  "two consecutive windows' mean launch time agree within 2 % "
+                                  "(steady state: a box still clearing a previous job's memory "
+                                  "runs the kernels slower for seconds), at most settle_max_s"},
             "ms_per_step": main_res["ms_per_step"],
             "gpu_clock_mhz": main_res["gpu_clock_mhz"],
             "higher_is_better": True,
