@@ -156,6 +156,9 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_XS
 #define F16_XS 1
 #endif
+#ifndef F16_PRIO
+#define F16_PRIO 0
+#endif
 // the lagged epilogue's lambdas forced inline (F16_LAMBDA_AI=0: the inliner
 // decides -- an A/B build for the ISA audit only, see DESIGN.md "k_frame16:
 // the two unexplained failures")
@@ -210,15 +213,43 @@ __device__ constexpr int brev(int k)
                    : (((k & 1) << 2) | (k & 2) | ((k & 4) >> 2));
 }
 
+// F16_PRIO (A/B builds): progress-balanced issue priority in k_frame16.  The
+// four waves of a SIMD issue oldest-first, so inside every barrier interval they
+// finish one after another (waves 0-3 / 4-7 / 8-11 / 12-15 of config 4's
+// forward pass 1: 1090 / 1610 / 2125 / 2690 cycles) and the last one runs
+// alone, without latency cover, while the others wait at the barrier.  Every
+// wave takes priority 3 after a barrier and lowers it at checkpoints inside the
+// interval's work (1: the middle of each DFT, of the split and of the Y build;
+// 2: every DFT stage), so a wave that is ahead yields issue to the ones behind
+template <int L>
+__device__ __forceinline__ void f16_prio()
+{
+#if F16_PRIO
+    __builtin_amdgcn_s_setprio(L);
+#endif
+}
+
 // in-place radix-2 DIF DFT-R (R = 8, 16) on the packed primitives: natural-order
 // input, X[k] ends in v[brev<R>(k)].  HZ: inputs R/2..R-1 are zero.  The
-// butterfly twiddle of span s is W_{2s}^j = W_32^{16 j / s}.
-template <int R, bool INV, bool HZ>
+// butterfly twiddle of span s is W_{2s}^j = W_32^{16 j / s}.  PM: k_frame16's
+// priority checkpoints (F16_PRIO)
+template <int R, bool INV, bool HZ, int PM = 0>
 __device__ __forceinline__ void dftp(f2 (&v)[R])
 {
     constexpr int LOG2R = R == 16 ? 4 : 3;
 #pragma unroll
     for (int st = 0; st < LOG2R; st++) {  // linear stage index: fully unrolled
+        if constexpr (PM == 1) {
+            if (st == LOG2R / 2)
+                f16_prio<1>();
+        } else if constexpr (PM == 2) {
+            if (st == 1)
+                f16_prio<2>();
+            else if (st == 2)
+                f16_prio<1>();
+            else if (st == 3)
+                f16_prio<0>();
+        }
         const int span = R >> (st + 1);
 #pragma unroll
         for (int start = 0; start < R; start += 2 * span) {
@@ -619,14 +650,25 @@ __device__ __forceinline__ void static_for(F &&f)
 #define F16_DIAG_FRAME 2
 #endif
 __device__ unsigned long long g_diag_f16[1 << 16];
+// ... and each wave's arrival at the stamped frame's barriers (g_diag_f16b,
+// NSTAMP per wave): arrival -> the next stamp is the wave's barrier wait
+__device__ unsigned long long g_diag_f16b[1 << 16];
 #define F16_MARK()                                       \
     do {                                                 \
         if (nst < NSTAMP - 3)                            \
             stamp[nst++] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define F16_PRE()                                        \
+    do {                                                 \
+        if (nar < NSTAMP)                                \
+            arrive[nar++] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define F16_MARK() \
     do {           \
+    } while (0)
+#define F16_PRE() \
+    do {          \
     } while (0)
 #endif
 
@@ -639,14 +681,17 @@ __device__ unsigned long long g_diag_f16[1 << 16];
 struct NoHook16 {
     __device__ void operator()(int) const {}
 };
+struct NoPre16 {  // pre_h(): right before each of the forward's barriers (diagnostic arrival stamps)
+    __device__ void operator()() const {}
+};
 // hook(2) / hook(3): called once every thread's pass-2 / pass-3 stores are
 // issued, before the pass's closing barrier (LDS-store-bound intervals whose
 // VALU is idle):
 // k_frame16's lagged epilogue runs the previous frame's outputs there
-template <int C, int WM, typename Mark, bool XS = false, typename Hook = NoHook16>
+template <int C, int WM, typename Mark, bool XS = false, typename Hook = NoHook16, typename Pre = NoPre16>
 __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const uint32_t *win, const uint32_t (&wr)[8],
                                                 f2 *buf, int *red, const f2 *tt, int tid, int g, int j, int pj,
-                                                int log2N, Mark mark, Hook hook = Hook())
+                                                int log2N, Mark mark, Hook hook = Hook(), Pre pre_h = Pre())
 {
     constexpr int T = C / 16, R1 = C / 256;
     const ColIdx<C, XS> cj(j);  // XS: pj is unused (the column reads / writes go through cj)
@@ -667,7 +712,9 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
     sum = group_sum_dpp(sum, 64);  // DPP moves to lane 63 (no LDS round trips)
     if ((tid & 63) == 63)
         red[tid >> 6] = sum;
+    pre_h();
     __syncthreads();
+    f16_prio<3>();
     mark();
     sum = 0;
 #pragma unroll
@@ -688,7 +735,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
         for (int s = 8; s < 16; s++)
             v[s] = f2{0.0f, 0.0f};
-        dftp<16, false, true>(v);
+        dftp<16, false, true, F16_PRIO>(v);
         // element 16 j + r: pidx = 17 j + r; xs = (16 j | (j & 15)) ^ r
         const int b1 = 16 * j | (j & 15);
 #pragma unroll
@@ -704,7 +751,7 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
             for (int r = 4; r < 8; r++)
                 u[r] = f2{0.0f, 0.0f};
-            dftp<8, false, true>(u);
+            dftp<8, false, true, F16_PRIO>(u);
             // element 8 (j + 128 h) + r (r < 8): pidx = 8 j + (j >> 1) + 1088 h + r;
             // xs = 1024 h + ((16 (j >> 1) | (8 (j & 1) ^ ((j >> 1) & 15))) ^ r)
             const int b2 = 16 * (j >> 1) | ((8 * (j & 1)) ^ ((j >> 1) & 15));
@@ -713,7 +760,9 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
                 buf[XS ? 1024 * h + (b2 ^ r) : 8 * j + (j >> 1) + 1088 * h + r] = u[brev<8>(r)];
         }
     }
+    pre_h();
     __syncthreads();
+    f16_prio<3>();
     mark();
     {
         const int k = j % R1;
@@ -723,8 +772,10 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
 #pragma unroll
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], F16_LD(tt + 512 + 16 * r + k));  // tw16h
-        dftp<16, false, false>(v);
+        dftp<16, false, false, F16_PRIO>(v);
+        pre_h();
         __syncthreads();
+        f16_prio<3>();
     mark();
         // element (j / R1) 16 R1 + k + R1 r.  pad: o mod 16 = k < R1, so
         // pidx(o + R1 r) = pidx(o) + R1 r + R1 r / 16.  xs: the lane part
@@ -738,8 +789,11 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
             buf[XS ? (lv ^ cr) : o + R1 * r + (R1 * r >> 4)] = v[brev<16>(r)];
         }
     }
+    f16_prio<3>();  // F16_PRIO: the lagged epilogue is the interval's critical path
     hook(2);
+    pre_h();
     __syncthreads();
+    f16_prio<3>();
     mark();
     {
 #pragma unroll
@@ -764,19 +818,24 @@ __device__ __forceinline__ void frame16_forward(const uint32_t (&w)[8], const ui
         for (int r = 1; r < 16; r++)
             v[r] = c_mul(v[r], c_mul(F16_LD(tt + 256 + 16 * r + (j & 15)), F16_LD(tt + 512 + 16 * r + (j >> 4))));  // twC
 #endif
-        dftp<16, false, false>(v);
+        dftp<16, false, false, F16_PRIO>(v);
         // the pass's stores go to exactly the 16 positions this thread read (its
         // column): no barrier between the reads and the stores (F16_P3_BAR=1: one)
 #if F16_P3_BAR
+        pre_h();
         __syncthreads();
+        f16_prio<3>();
 #endif
     mark();
 #pragma unroll
         for (int q = 0; q < 16; q++)  // Z[j + T q] back into the slot
             buf[XS ? cj.at(q) : pj + po(T * q)] = v[brev<16>(q)];
     }
+    f16_prio<3>();
     hook(3);
+    pre_h();
     __syncthreads();
+    f16_prio<3>();
     mark();
 }
 
@@ -1415,7 +1474,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #ifdef TDOA_DIAG
     constexpr int NSTAMP = 48;  // k_frame16: up to 45 phase marks (config 4: 33)
     unsigned long long stamp[NSTAMP] = {};
-    int nst = 0;
+    unsigned long long arrive[NSTAMP] = {};
+    int nst = 0, nar = 0;
     const int64_t diag_fr = blockIdx.x + (B >= (int64_t)(F16_DIAG_FRAME + 1) * gridDim.x ? F16_DIAG_FRAME : 0) *
                                              (int64_t)gridDim.x;
 #else
@@ -1479,18 +1539,22 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (fr == diag_fr)
             F16_MARK();  // the forward's barriers (diagnostic build)
     };
+    auto fwd_pre = [&] {
+        if (fr == diag_fr)
+            F16_PRE();  // ... and the waves' arrivals at them
+    };
     if constexpr (ELAG) {
         auto lag_hook = [&](int ps) F16_AI {
             if (prev >= 0)
                 epi16(prev, ps);  // the previous frame's outputs (scl holds its scores until round 0's pass 3)
         };
-        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS, decltype(lag_hook)>(
-            w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N, fwd_mark, lag_hook);
+        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS, decltype(lag_hook), decltype(fwd_pre)>(
+            w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N, fwd_mark, lag_hook, fwd_pre);
         if (prev >= 0)
             gate_of(prev);  // its lags are in lagl since the forward's closing barrier
     } else {
-        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS>(w, f16_win_lds<C>() ? winl : win, wr, buf, red,
-                                                                        tt, tid, g, j, pj, kp.log2N, fwd_mark);
+        frame16_forward<C, f16_win_mode<C>(), decltype(fwd_mark), XS, NoHook16, decltype(fwd_pre)>(
+            w, f16_win_lds<C>() ? winl : win, wr, buf, red, tt, tid, g, j, pj, kp.log2N, fwd_mark, NoHook16(), fwd_pre);
     }
     if (fr == diag_fr)
         F16_MARK();  // forward transforms done
@@ -1523,6 +1587,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             Un[m][s] = c_unit(c_conj_add_i(e, od), e2);
         }
     }
+    if constexpr (F16_PRIO != 0)
+        f16_prio<2>();  // split done (F16_PRIO checkpoint)
     if (tid < M) {  // X[C/2] = conj(Z[C/2]) (x2): self-paired bin
         const f2 zh = bufs[tid * BUF + lidx<XS>(C / 2)];
         xhalf[tid] = c_unit(f2{2.0f * zh.x, -2.0f * zh.y}, e2);
@@ -1532,7 +1598,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // slot), and position C / 2 -- read for X[C/2] by threads 0 .. M - 1, stored
     // by thread 0 -- stays inside wave 0, whose LDS operations are in order
 #if F16_SPLIT_BAR
+    if (fr == diag_fr)
+        F16_PRE();
     __syncthreads();  // slots consumed: they become the pairs' buffers
+    f16_prio<3>();
 #endif
     if (fr == diag_fr)
         F16_MARK();  // unit spectra in registers
@@ -1560,6 +1629,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // packed inverse input Y of pair p0 + gg into buffer gg (all threads)
         static_for<0, G>([&](auto gc) {
             constexpr int pc = p0 + decltype(gc)::value;
+            if constexpr (F16_PRIO != 0 && decltype(gc)::value == G / 2)
+                f16_prio<1>();
             if constexpr (pc < P) {
                 constexpr int pi = pair_first<M>(pc), pj = pair_second<M>(pc);
                 f2 *yb = bufs + decltype(gc)::value * BUF;
@@ -1578,7 +1649,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 }
             }
         });
+        if (fr == diag_fr)
+            F16_PRE();
         __syncthreads();
+        f16_prio<3>();
         if (fr == diag_fr)
             F16_MARK();  // the round's Y buffers written
         const int p = p0 + g;
@@ -1592,7 +1666,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 v[r] = F16_LD(buf + (XS ? cjl.at(r) : pjl + po(T * r)));
-            dftp<16, true, false>(v);
+            dftp<16, true, false, F16_PRIO>(v);
         }
         // FG, last round: the idle groups' waves solve the previous frame's grid
         constexpr bool FGL = FG && decltype(rc)::value == ROUNDS - 1;
@@ -1602,7 +1676,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             if (!on && fgr)
                 fgg.levels(pgw, gw, gln, fqr);  // seg A
         }
+        if (fr == diag_fr)
+            F16_PRE();
         __syncthreads();
+        f16_prio<3>();
         if (fr == diag_fr)
             F16_MARK();
         if (on) {
@@ -1615,7 +1692,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
             if (!on && fgr)
                 fgg.bounds(pgw, gw, gln, fqr);  // seg B
         }
+        if (fr == diag_fr)
+            F16_PRE();
         __syncthreads();
+        f16_prio<3>();
         if (fr == diag_fr)
             F16_MARK();
         // pass 2: outputs r'' in {0, 1, 14, 15} only
@@ -1625,6 +1705,8 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         if (on)
 #pragma unroll
         for (int r = 0; r < 4; r++) {  // inputs r, r + 4, r + 8, r + 12 at a time
+            if (r == 2)
+                f16_prio<1>();
             f2 l0 = F16_LD(buf + (XS ? cjl.at(r) : pjl + po(T * r)));
             f2 l1 = F16_LD(buf + (XS ? cjl.at(r + 4) : pjl + po(T * (r + 4))));
             const f2 h0 = c_mulconj(F16_LD(buf + (XS ? cjl.at(r + 8) : pjl + po(T * (r + 8)))), F16_TW256(r + 8));
@@ -1650,8 +1732,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         // jl + T c for output c), positions no other thread reads in this pass:
         // no barrier between the pass's reads and its stores.  Padded layout:
         // element 64 a + 16 c + k (a = jl >> 4), after a barrier
-        if constexpr (!XS)
+        if constexpr (!XS) {
+            if (fr == diag_fr)
+                F16_PRE();
             __syncthreads();
+            f16_prio<3>();
+        }
         if (fr == diag_fr)
             F16_MARK();
         if (on) {
@@ -1674,7 +1760,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                 fgl.cand[gw] = fgc;
             }
         }
+        if (fr == diag_fr)
+            F16_PRE();
         __syncthreads();
+        f16_prio<3>();
         if (fr == diag_fr)
             F16_MARK();
         // pass 3 by one wave of the group, one output per column.  Waves of a
@@ -1735,7 +1824,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                     fgl.key[FG_NGW + gw] = kk;
             }
         }
+        if (fr == diag_fr)
+            F16_PRE();
         __syncthreads();  // the buffers are rewritten by the next round
+        f16_prio<3>();
         if (fr == diag_fr)
             F16_MARK();
     });
@@ -1771,7 +1863,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                                 ep_w, ep_off, fgw);
         }
         if constexpr (!ELAG) {
+            if (fr == diag_fr)
+                F16_PRE();
             __syncthreads();  // lagl complete for the gate; scl free for the next frame
+            f16_prio<3>();
             if (fr == diag_fr)
                 F16_MARK();
         }
@@ -1838,8 +1933,10 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     }
 #ifdef TDOA_DIAG
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 64)
-        for (int i = 0; i < NSTAMP; i++)
+        for (int i = 0; i < NSTAMP; i++) {
             g_diag_f16[(blockIdx.x * 16 + (threadIdx.x >> 6)) * NSTAMP + i] = stamp[i];
+            g_diag_f16b[(blockIdx.x * 16 + (threadIdx.x >> 6)) * NSTAMP + i] = arrive[i];
+        }
 #endif
 }
 #undef F16_MARK
@@ -2493,6 +2590,15 @@ int tdoa_launch_phat_r16(const tdoa_kparams &kp, const tdoa_kout &out, const int
 }
 
 #ifdef TDOA_DIAG
+extern "C" int tdoa_diag_fetch_f16b(unsigned long long *host, int n)
+{
+    if (n > (1 << 16))
+        n = 1 << 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_f16b), sizeof(unsigned long long) * n, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
 extern "C" int tdoa_diag_fetch_f16(unsigned long long *host, int n)
 {
     if (n > (1 << 16))
