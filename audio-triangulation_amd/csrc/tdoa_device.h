@@ -106,6 +106,84 @@ __device__ __forceinline__ uint4 ring_chunk(const tdoa_kparams &kp, int64_t slot
     return ring_chunk(kp, ring_slot(kp, slot), m, k);
 }
 
+struct NoBetween {
+    __device__ void operator()() const {}
+};
+
+// Three mics (config 5's streaming batch), a thread's CH chunks c0 + nt i at
+// once: every chunk's slot records are requested first, then every chunk's
+// ring words, then the bytes are picked -- two dependent round trips after the
+// batch count.  Chunk by chunk (ring_chunk), each chunk's record loads and word
+// loads sat under the chunk's own branch and were waited on in turn: six round
+// trips for three chunks.  between() runs once the records are requested and
+// before their values are used (the EMA states' loads go there: their stream
+// ids were requested with the records).  Chunks >= nchunk read chunk nchunk - 1's
+// words and come back zero; the rare chunks that start before the stream or
+// wrap the ring take ring_chunk's byte path.
+template <int CH, typename Between>
+__device__ __forceinline__ void ring_chunks3(const tdoa_kparams &kp, int64_t f0, int c0, int nt, int nchunk, int cpr,
+                                             uint4 (&v)[CH], Between between)
+{
+    const int64_t cl = kp.ring_len;
+    int sid[CH];
+    int64_t fe[CH], fa[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+        const int c = c0 + nt * i < nchunk ? c0 + nt * i : nchunk - 1;
+        const int64_t slot = f0 + (c / cpr) / 3;
+        sid[i] = kp.frame_ids[slot];
+        fe[i] = kp.frame_end[slot];
+        fa[i] = kp.frame_ring_at[slot];
+    }
+    between();
+    uint32_t wd[CH][7], sh[CH];
+    bool fast[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+        const int c = c0 + nt * i < nchunk ? c0 + nt * i : nchunk - 1;
+        const int r = c / cpr, k = c - r * cpr, m = r - (r / 3) * 3;
+        const int64_t t0 = fe[i] - kp.N + 8 * k;
+        int64_t j = fa[i] + 8 * k;
+        if (j >= cl)
+            j -= cl;
+        fast[i] = t0 >= 0 && j + 10 <= cl;
+        // (a slow chunk reads its stream's first words instead: in bounds, unused)
+        const uint8_t *ab = kp.frame_ring + (size_t)sid[i] * cl * 3 + m + (fast[i] ? j : 0) * 3;
+        sh[i] = (uint32_t)((uintptr_t)ab & 3u);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(ab - sh[i]);
+#pragma unroll
+        for (int d = 0; d < 7; d++)
+            wd[i][d] = wp[d];
+    }
+    // every chunk's words requested before the first pick waits on any (the
+    // scheduler otherwise pulled chunk 0's picks, and a full wait, ahead of
+    // chunks 1 and 2's address arithmetic)
+    __builtin_amdgcn_sched_barrier(0);
+    // (the picks unconditional: under the chunk's branch, the compiler sank the
+    // chunk's loads into it, one round trip per chunk again)
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+        const int c = c0 + nt * i;
+        uint32_t x[6];
+#pragma unroll
+        for (int d = 0; d < 6; d++)
+            x[d] = __builtin_amdgcn_alignbyte(wd[i][d + 1], wd[i][d], sh[i]);
+        // sample s is byte 3 s of the aligned words (ring_chunk's fast path)
+        uint4 q = make_uint4(__builtin_amdgcn_perm(0u, x[0], 0x0C030C00u), __builtin_amdgcn_perm(x[2], x[1], 0x0C050C02u),
+                             __builtin_amdgcn_perm(x[3], x[3], 0x0C030C00u), __builtin_amdgcn_perm(x[5], x[4], 0x0C050C02u));
+        if (!fast[i] && c < nchunk) {
+            // the records read again (rare path): holding them across the
+            // word loads cost registers the kernel does not have (an opaque
+            // slot index: not merged with the first loads)
+            const int r = c / cpr, k = c - r * cpr;
+            int64_t slot = f0 + r / 3;
+            asm volatile("" : "+v"(slot));
+            q = ring_chunk(kp, slot, r - (r / 3) * 3, k);
+        }
+        v[i] = c < nchunk ? q : make_uint4(0, 0, 0, 0);
+    }
+}
+
 typedef short v2s __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c)

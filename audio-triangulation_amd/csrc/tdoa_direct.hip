@@ -39,9 +39,19 @@ __device__ unsigned long long g_diag[1 << 20];
                 __builtin_amdgcn_s_memtime();                           \
     } while (0)
 #define TDOA_GRID_MARK(i) DIAG_STAMP(i)
+// the constant 100 MHz clock (one base for every CU): slots 11 / 12
+#define DIAG_RT(i)                                                      \
+    do {                                                                \
+        if (threadIdx.x == 0)                                           \
+            g_diag[(size_t)blockIdx.x * TDOA_DIAG_SLOTS + (i)] =        \
+                __builtin_amdgcn_s_memrealtime();                       \
+    } while (0)
 #else
 #define DIAG_STAMP(i) \
     do {              \
+    } while (0)
+#define DIAG_RT(i) \
+    do {           \
     } while (0)
 #endif
 
@@ -248,7 +258,7 @@ __device__ void grid_mf(const tdoa_kparams &kp, const int64_t *scores, uint64_t 
 // grid solve runs on (vga_heatmap.h reads corr_*) -- and the EMA argmax per
 // pair (ema_best).  The clock now = end * 10^6 / fs.  Replaces k_stream_update's
 // per-slot pass for the shapes this kernel solves (no fresh-score round trip).
-// The stream states are requested at the kernel's start (ema_prefetch: the
+// The stream states are requested at the kernel's start (ema_ids / ema_states: the
 // thread's EMA_E elements of the workgroup's [F][P][K] block), so their HBM
 // latency hides behind the staging and the xcorr.
 // the streaming kernel's grid tables requested after the xcorr (see k_direct_mfma;
@@ -266,8 +276,25 @@ struct EmaPre {
     int64_t ev[EMA_E];
 };
 
-__device__ __forceinline__ EmaPre ema_prefetch(const tdoa_kparams &kp, const tdoa_stream_params &sp,
-                                               int64_t f0, int nf)
+// in two steps: the stream ids (requested with the staging's slot records),
+// then the states.  Clamped, unguarded loads: a guarded load is a branch the
+// wait-count pass cannot look through (one round trip per element)
+struct EmaIds {
+    int sid[EMA_E];
+};
+__device__ __forceinline__ EmaIds ema_ids(const tdoa_kparams &kp, const tdoa_stream_params &sp, int64_t f0, int nf)
+{
+    EmaIds e;
+    const int PK = kp.P * kp.K;
+#pragma unroll
+    for (int i = 0; i < EMA_E; i++) {
+        const int f = ((int)threadIdx.x + i * (int)blockDim.x) / PK;
+        e.sid[i] = sp.ids[f0 + (f < nf ? f : nf - 1)];
+    }
+    return e;
+}
+__device__ __forceinline__ EmaPre ema_states(const tdoa_kparams &kp, const tdoa_stream_params &sp, const EmaIds &ids,
+                                             int nf)
 {
     EmaPre e;
     const int PK = kp.P * kp.K;
@@ -275,7 +302,8 @@ __device__ __forceinline__ EmaPre ema_prefetch(const tdoa_kparams &kp, const tdo
     for (int i = 0; i < EMA_E; i++) {
         const int x = (int)threadIdx.x + i * (int)blockDim.x;
         const int f = x / PK;
-        e.ev[i] = f < nf ? sp.est[(size_t)sp.ids[f0 + f] * PK + (x - f * PK)] : 0;
+        const int64_t v = sp.est[(size_t)ids.sid[i] * PK + (f < nf ? x - f * PK : 0)];
+        e.ev[i] = f < nf ? v : 0;
     }
     return e;
 }
@@ -387,9 +415,12 @@ struct MfTabs {
 // WS: the workgroup's thread count is a multiple of the chunks per row, so
 // every chunk of a thread sits at the same row offset and reads the same
 // window chunk: one window load per thread (8 registers fewer per chunk)
-template <bool PREPARED, int CH, bool WS = false>
+// between(): once the frames' first loads are requested (ring_chunks3) -- the
+// streaming kernel's EMA state loads
+template <bool PREPARED, int CH, bool WS = false, typename Between = NoBetween>
 __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm, char *smem, const MfTabs &tb,
-                                         const int16_t *__restrict__ frames, int64_t f0, int nf)
+                                         const int16_t *__restrict__ frames, int64_t f0, int nf,
+                                         Between between = Between())
 {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int rows = nf * kp.M, NW = kp.N / 2, padw = kp.PADW, RS = kp.RS;
@@ -404,6 +435,10 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
         if (!PREPARED)
             w[0] = reinterpret_cast<const uint4 *>(kp.window)[tid % cpr];
     }
+    if (WS && CH <= 3 && kp.frame_ring && kp.M == 3) {
+        ring_chunks3<CH>(kp, f0, tid, nt, nchunk, cpr, v, between);
+    } else {
+    between();
 #pragma unroll
     for (int i = 0; i < CH; i++) {
         const int c = tid + nt * i;
@@ -424,6 +459,7 @@ __device__ __forceinline__ void stage_mf(const tdoa_kparams &kp, const Smem &sm,
                 if (!PREPARED)
                     w[i] = reinterpret_cast<const uint4 *>(kp.window)[k];
         }
+    }
     }
     // the prior: requested now, written once the frames have arrived
     const float pr = tid < kp.K ? kp.prior[tid] : 0.0f;
@@ -521,6 +557,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     const Smem sm = carve(smem, kp, blockDim.x >> 6);
     const int64_t f0 = (int64_t)blockIdx.x * kp.F;
     DIAG_STAMP(10);
+    DIAG_RT(11);
     if (count) {  // batch size known on the device only (streaming pipeline)
         // at most B slots (one per stream): a corrupted counter is clamped
         // before any reader (ema_hop's stats, the batch bound) sees it
@@ -552,9 +589,15 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     if constexpr (KEYGRID && !(EMA && MF_EMA_LATE_TABLES))
         grid_tables();
     EmaPre epre{};
+    EmaIds eids{};
     if constexpr (EMA)
-        epre = ema_prefetch(kp, ef.sp, f0, nf);
-    stage_mf<PREPARED, CH, EMA>(kp, sm, smem, tb, frames, f0, nf);  // EMA launches: threads % (N / 8) == 0
+        eids = ema_ids(kp, ef.sp, f0, nf);
+    // EMA launches: threads % (N / 8) == 0; their states are requested as soon
+    // as the ids are in (with the slot records)
+    stage_mf<PREPARED, CH, EMA>(kp, sm, smem, tb, frames, f0, nf, [&]() __attribute__((always_inline)) {
+        if constexpr (EMA)
+            epre = ema_states(kp, ef.sp, eids, nf);
+    });
     DIAG_STAMP(1);
     DIAG_STAMP(2);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
@@ -650,6 +693,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
             grid_phase_t<int64_t, 4, TWC>(kp, sm.scores, sm.redv, sm.redi, out, f0, nf, nullptr, nullptr, omask);
     }
     DIAG_STAMP(5);
+    DIAG_RT(12);
 }
 
 // --------------------------------------------------------------- EMA
@@ -922,6 +966,25 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
         if (grid > INT_MAX)
             return tdoa_set_error(-1, "DIRECT: batch too large for one launch");
         hipStream_t st = (hipStream_t)stream;
+        // A/B library only, a measurement: TDOA_DIRECT_RESGRID=1 launches the
+        // streaming EMA kernel on the resident workgroups only -- what the
+        // launch's empty workgroups (one per possible batch; ~3.4 k of 16384
+        // streams trigger at config 5) cost.  Wrong once a hop triggers more
+        // frames than the grid holds, so never in the product
+        auto dev_grid = [&](const void *fn) -> unsigned {
+#if TDOA_AB
+            static const bool res_grid = [] {
+                const char *e = getenv("TDOA_DIRECT_RESGRID");
+                return e && *e && e[0] != '0';
+            }();
+            if (res_grid && count_dev) {
+                const int res = tdoa_resident_blocks(fn, threads, lds);
+                return (unsigned)(res > 0 && res < grid ? res : grid);
+            }
+#endif
+            (void)fn;
+            return (unsigned)grid;
+        };
         constexpr int TWX = (TDOA_MAX_PAIRS + 3) / 4;
         const tdoa_stream_fuse ef = ema ? *ema : tdoa_stream_fuse{};
         if (ema && (!count_dev || prepared))
@@ -930,10 +993,11 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
             return tdoa_set_error(-1, "DIRECT: EMA state of a workgroup exceeds its prefetch registers");
 #define TDOA_LAUNCH_MF(PREP, TWC, CH)                                                                          \
     do {                                                                                                       \
-        if (ema)                                                                                               \
-            hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH, !PREP>), dim3((unsigned)grid), dim3(threads), lds, \
+        if (ema) {                                                                                             \
+            const void *fn = (const void *)k_direct_mfma<PREP, TWC, CH, !PREP>;                                \
+            hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH, !PREP>), dim3(dev_grid(fn)), dim3(threads), lds,  \
                                st, kp, out, frames, B, count_dev, n0, nq, tb, ef);                             \
-        else                                                                                                   \
+        } else                                                                                                 \
             hipLaunchKernelGGL((k_direct_mfma<PREP, TWC, CH, false>), dim3((unsigned)grid), dim3(threads),     \
                                lds, st, kp, out, frames, B, count_dev, n0, nq, tb, ef);                        \
     } while (0)

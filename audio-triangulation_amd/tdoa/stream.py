@@ -19,8 +19,11 @@ from .localizer import Localizer
 
 
 class StreamPipeline:
+    # use_graph: each hop replayed as a captured hipGraph of its two kernels.
+    # Plain stream launches are the default: 67.0 vs 71.8 us per config-5 hop
+    # (tools/diag_stream_launch.py, same box; the graph's launch adds ~5 us)
     def __init__(self, loc: Localizer, capture: torch.Tensor, hop: int = 512,
-                 use_graph: bool = True):
+                 use_graph: bool = False):
         if loc.engine != "direct":
             raise ValueError("the streaming pipeline runs the DIRECT engine")
         if capture.dtype != torch.uint8 or capture.dim() != 3 or capture.shape[2] != loc.dims.M:

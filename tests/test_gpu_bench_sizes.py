@@ -108,7 +108,7 @@ def test_bench_size_stream(oracle):
                            device=torch.device("cuda", 0))
     torch.cuda.synchronize()
     pick = np.linspace(0, S - 1, 64).round().astype(np.int64)
-    pipe = StreamPipeline(loc, cap, hop=H, use_graph=True)
+    pipe = StreamPipeline(loc, cap, hop=H)  # bench.py's launch form
     recs = {int(s): [] for s in pick}
     total = 0
     for _ in range(hops):

@@ -49,9 +49,11 @@ print("  before stage: count read %d cyc; stage split: issue+zero %d, frame data
        np.median(st[:, 1] - st[:, 7])))
 print("  grid split: scan %d, reductions %d, final %d cyc (median)" %
       (np.median(st[:, 8] - st[:, 4]), np.median(st[:, 9] - st[:, 8]), np.median(st[:, 5] - st[:, 9])))
-t0 = st[:, 0] - st[:, 0].min()
-te = st[:, 5] - st[:, 0].min()
-print("  launch span %d cyc" % te.max())
-print("  workgroup start: p25 %d p50 %d p75 %d p90 %d max %d" % tuple(np.percentile(t0, [25, 50, 75, 90, 100])))
-print("  workgroup end:   p25 %d p50 %d p75 %d p90 %d max %d" % tuple(np.percentile(te, [25, 50, 75, 90, 100])))
+# s_memtime has no common base across CUs: start / end of every workgroup
+# from the 100 MHz realtime stamps (slots 11, 12) relative to the first start
+r0 = st[:, 11].min()
+rs, re_ = (st[:, 11] - r0) * 10.0, (st[:, 12] - r0) * 10.0  # ns
+print("  realtime (ns from the first workgroup's start): start p50 %.0f p90 %.0f max %.0f; end p10 %.0f p50 %.0f p90 %.0f max %.0f"
+      % (np.median(rs), np.percentile(rs, 90), rs.max(), np.percentile(re_, 10), np.median(re_), np.percentile(re_, 90), re_.max()))
+print("  workgroup duration (realtime) p50 %.0f ns max %.0f ns" % (np.median(re_ - rs), (re_ - rs).max()))
 pipe.close()
