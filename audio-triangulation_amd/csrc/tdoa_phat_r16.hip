@@ -159,6 +159,16 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_PRIO
 #define F16_PRIO 0
 #endif
+// the round's Y[C/2] values: lane-parallel in wave 0 (1) or thread 0 per pair (0):
+// config 4 83.7-84.0 vs 85.8-85.9 ms, config 3 3.270-3.277 vs 3.294-3.303 ms per
+// step (same box)
+#ifndef F16_YHALF
+#define F16_YHALF 1
+#endif
+// the gate's sum of squared lags at P > 16: wave 0's lanes + a DPP sum (1) or thread 0 (0)
+#ifndef F16_GATEW
+#define F16_GATEW 1
+#endif
 // the lagged epilogue's lambdas forced inline (F16_LAMBDA_AI=0: the inliner
 // decides -- an A/B build for the ISA audit only, see DESIGN.md "k_frame16:
 // the two unexplained failures")
@@ -1452,11 +1462,23 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
         }
     };
     auto gate_of = [&](int64_t f) F16_AI {
-        if (threadIdx.x == 0 && out.gate) {
+        // P > 16: wave 0's lanes one lag each, a DPP sum -- thread 0 alone read
+        // and summed config 4's 28 lags one after another (83.2 vs 84.0 ms per
+        // step, same box; at config 3's 6 lags the DPP sum cost more: 3.300 vs
+        // 3.273 ms)
+        if (F16_GATEW && P > 16 && threadIdx.x < 64 && out.gate) {
+            const int ln = (int)threadIdx.x;
+            int tot = 0;
+            for (int q = ln; q < P; q += 64)
+                tot += lagl[q] * lagl[q];
+            tot = group_sum_dpp(tot, 64);
+            if (ln == 63)
+                out.gate[f] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+        } else if ((!F16_GATEW || P <= 16) && threadIdx.x == 0 && out.gate) {
             int tot = 0;
             for (int q = 0; q < P; q++)
                 tot += lagl[q] * lagl[q];
-            out.gate[f] = tot > 4 ? 1 : 0;  // sample_compute.h:124-134
+            out.gate[f] = tot > 4 ? 1 : 0;
         }
     };
     // DM 1: the epilogue's pairs w, w + 16
@@ -1643,12 +1665,30 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
                     yb[yb0[s]] = c_add_i(ss, qq);
                     yb[yb1[s]] = c_conj_add_mi(ss, qq);
                 }
-                if (tl == 0) {  // Y[C/2] from R[C/2] alone
+                if (!F16_YHALF && tl == 0) {  // Y[C/2] from R[C/2] alone
                     const f2 Rh = c_conjmul(xhalf[pi], xhalf[pj]);
                     yb[lidx<XS>(C / 2)] = c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), twh));
                 }
             }
         });
+#if F16_YHALF
+        // Y[C/2] of the round's pairs, lane gg of wave 0 for pair p0 + gg: one
+        // branch instead of one per pair on thread 0 (wave 0 ran ~1.1 k cycles
+        // longer than its SIMD's other waves in every Y interval).  Wave 0 as
+        // before: its LDS operations are in order -- X[C/2] (xhalf) was written by
+        // its threads 0 .. M - 1 after they read Z[C/2] at the positions
+        // written here, and thread 0's stores above put the partner value there first
+        if (tl < G && p0 + tl < P) {
+            const int pc = p0 + tl;
+            int pi = 0, q = pc;
+            while (q >= M - 1 - pi) {  // pair_first / pair_second at run time
+                q -= M - 1 - pi;
+                pi++;
+            }
+            const f2 Rh = c_conjmul(xhalf[pi], xhalf[pi + 1 + q]);
+            bufs[tl * BUF + lidx<XS>(C / 2)] = c_add_i(c_addconj(Rh, Rh), c_mulconj(c_subconj(Rh, Rh), twh));
+        }
+#endif
         if (fr == diag_fr)
             F16_PRE();
         __syncthreads();

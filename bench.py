@@ -77,7 +77,7 @@ CONFIGS = {
             M=8, N=2048, mics="circle", batch=1_000_000, scaling="strong"),
     # batch = streams per GPU; one step = one 512-sample hop of every stream
     5: dict(desc="BASELINE config 5: streaming 48 kHz, 512-sample hop, 3-mic triangle, "
-                 "trigger + DIRECT xcorr + EMA + grid, one hipGraph per hop",
+                 "trigger + DIRECT xcorr + EMA + grid, two stream launches per hop",
             M=3, N=1024, mics=None, batch=16384, fs=48000, hop=512, scaling="weak"),
 }
 
@@ -863,7 +863,7 @@ def main_stream(args, dev, ri, cache):
                          "frac": res["capture_bytes_per_step"] / ri.world / (res["kernel_ms"] * 1e-3) / 1e9
                          / HBM_PEAK_GBS,
                          **dict(zip(("traffic", "traffic_source"), stream_traffic(args))),
-                         "kernel": "all kernels of a hop (hipGraph)", "kernel_ms": res["kernel_ms"],
+                         "kernel": "all kernels of a hop (trigger + DIRECT)", "kernel_ms": res["kernel_ms"],
                          "bytes_per_step": res["capture_bytes_per_step"] // ri.world,
                          # what the sliding trigger must read per hop: the half-window
                          # sums after every sample need the entering sample (this hop),
