@@ -169,6 +169,12 @@ __device__ __forceinline__ void sts2(f2 *buf, int i, f2 v) { buf[pidx(i)] = v; }
 #ifndef F16_GATEW
 #define F16_GATEW 1
 #endif
+// the four-pairs epilogue's pairs spread over a multiple of four waves
+// (f16_epi_pair).  A/B: config 4 82.8-83.0 vs 82.7-82.9 ms (neutral), config 3
+// 3.309 vs 3.279-3.285 ms (slower), same box -- default 0, the packed map
+#ifndef F16_EPI_SPREAD
+#define F16_EPI_SPREAD 0
+#endif
 // the lagged epilogue's lambdas forced inline (F16_LAMBDA_AI=0: the inliner
 // decides -- an A/B build for the ISA audit only, see DESIGN.md "k_frame16:
 // the two unexplained failures")
@@ -617,6 +623,26 @@ __device__ __forceinline__ int opaque_idx(int t)
 {
     asm volatile("" : "+v"(t));
     return t;
+}
+
+// the four-pairs epilogue's lane -> pair map (frame16_out16: a 16-lane row per
+// pair): packed, wave w row q = pair 4 w + q (waves 0 .. 6 at config 4: SIMDs
+// 0-2 get eight pairs, SIMD 3 four); F16_EPI_SPREAD=1 (A/B): EW = ceil(P / 4)
+// rounded up to a multiple of four waves, wave w < EW row q takes pair w + EW q,
+// equal shares per SIMD (measured no faster).
+// P: the lane has no pair
+template <int P>
+__device__ __forceinline__ constexpr int f16_epi_waves()
+{
+    return F16_EPI_SPREAD ? ((((P + 3) / 4 + 3) & ~3) < 16 ? (((P + 3) / 4 + 3) & ~3) : 16) : (P + 3) / 4;
+}
+template <int P>
+__device__ __forceinline__ int f16_epi_pair(int t)
+{
+    constexpr int EW = f16_epi_waves<P>();
+    const int w = t >> 6, q = (t >> 4) & 3;
+    const int p = F16_EPI_SPREAD ? w + EW * q : 4 * w + q;
+    return w < EW && p < P ? p : P;
 }
 
 // pairs in the host's lexicographic order (tdoa_capi.cpp): pair p = (i, j)
@@ -1402,7 +1428,7 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     // forward's registers peak)
     uint32_t e16_rng = 0;
     if constexpr (OUT16) {
-        const int e16_p = (int)threadIdx.x >> 4;  // wave w, row q: pair 4 w + q
+        const int e16_p = f16_epi_pair<P>((int)threadIdx.x);  // this lane's row's pair
         const int pq = e16_p < P ? e16_p : 0;
         // per-lane loads, waited for below.  Workaround for a codegen bug: picking
         // each row's range from the wave's four scalar loads (F16_RNG_SCALAR=1)
@@ -1446,12 +1472,12 @@ __global__ void __launch_bounds__(1024, 1) k_frame16(tdoa_kparams kp, tdoa_kout 
     constexpr bool ELAG = OUT16 && F16_EPI_LAG != 0;
     // the waves (four pairs each) whose outputs run after the forward's pass-2
     // stores; the rest after its pass-3 stores (F16_EPI_SPLIT: -1 half, else count)
-    constexpr int EPW = (P + 3) / 4, EPS = F16_EPI_SPLIT < 0 ? EPW / 2 : (F16_EPI_SPLIT < EPW ? F16_EPI_SPLIT : EPW);
+    constexpr int EPW = f16_epi_waves<P>(), EPS = F16_EPI_SPLIT < 0 ? EPW / 2 : (F16_EPI_SPLIT < EPW ? F16_EPI_SPLIT : EPW);
     auto epi16 = [&](int64_t f, int ps) F16_AI {
         const int t = opaque_idx((int)threadIdx.x);
-        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = t >> 4;
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), pe = f16_epi_pair<P>(t);
         const bool mine = ps == 0 || (ps == 2 ? wv < EPS : wv >= EPS);
-        if (!F16_NO_OUT && mine && 4 * wv < P && pe < P) {
+        if (!F16_NO_OUT && mine && wv < f16_epi_waves<P>() && pe < P) {
             const int r = t & 15, lo = (int)(e16_rng & 0xFFu), wd = (int)((e16_rng >> 8) & 0xFFu),
                       of = (int)(e16_rng >> 16);
             constexpr bool SPL = F16_OUT16_LOOPS != 0;

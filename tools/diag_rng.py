@@ -5,6 +5,10 @@ with -DF16_RNG_DUMP over the first 1024 lag slots, against the host's kp.wc_*
 (recomputed here from the LUT as tdoa_capi.cpp does).
 
     TDOA_LIB=.../libtdoa_X.so python3 tools/diag_rng.py [3|4]
+
+The lane -> pair map is k_frame16's f16_epi_pair: packed (the default) or,
+with EPI_SPREAD=1 in the environment here for a -DF16_EPI_SPREAD=1 build,
+spread over a multiple of four waves.
 """
 import os
 import sys
@@ -34,8 +38,11 @@ torch.cuda.synchronize()
 got = out["lags"].reshape(-1)[:1024].cpu().numpy().astype(np.uint32)
 bad = 0
 rows = set()
+spread = os.environ.get("EPI_SPREAD", "0") != "0"
+EW = min(16, (((P + 3) // 4 + 3) & ~3)) if spread else (P + 3) // 4
 for t in range(1024):
-    p = t >> 4
+    wv, q = t >> 6, (t >> 4) & 3
+    p = (wv + EW * q if spread else 4 * wv + q) if wv < EW else P
     if p >= P:
         continue
     exp = int(lo[p]) | int(w[p]) << 8 | int(off[p]) << 16
