@@ -604,11 +604,36 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
     const int *rsum = reinterpret_cast<const int *>(smem + tb.rsum);
     const int RS = kp.RS;
 
-    const int g = lane >> 4, r = lane & 15, rr = r < nq ? r : nq - 1;
+    const int g = lane >> 4, r = lane & 15;
     const int K = kp.K, S = kp.S, P = kp.P, NB = kp.N / 64 + 1;
-    for (int it = wave; it < nf * P; it += nwaves) {
-        const int f = it / P, p = it - f * P;
-        const int rowa = f * kp.M + kp.pair_i[p], rowb = f * kp.M + kp.pair_j[p];
+    // xcorr units.  Per pair (a, b): the tile's 16 rows are a's fine shifts, its
+    // columns b's coarse 16-lag blocks, nq of them used.  xc3 (three mics, 2 nq
+    // <= 16): per (frame, first mic a) -- a = 0 puts pairs (0,1) and (0,2) side by
+    // side (columns 0 .. nq - 1 mic 1, nq .. 2 nq - 1 mic 2), a = 1 pair (1,2):
+    // two tiles per frame instead of three, and the streaming workgroup's eight
+    // waves take F = 4 frames' eight units in one pass (twelve units took two)
+    const bool xc3 = kp.xc3 != 0;
+    const int nu = xc3 ? 2 * nf : nf * P;
+    for (int it = wave; it < nu; it += nwaves) {
+        const int f = xc3 ? it >> 1 : it / P;
+        const int ma = xc3 ? it & 1 : kp.pair_i[it - f * P];
+        // this lane's column: pair p, partner row, coarse block cb (< nq: valid)
+        int p, mb, cb;
+        bool valid;
+        if (xc3) {
+            const int two = ma == 0 && r >= nq;  // a = 0: the second partner's columns
+            const int c = r - two * nq;
+            valid = c < nq;
+            cb = c < nq ? c : nq - 1;
+            p = ma == 0 ? two : 2;
+            mb = ma == 0 ? 1 + two : 2;
+        } else {
+            p = it - f * P;
+            mb = kp.pair_j[p];
+            valid = r < nq;
+            cb = r < nq ? r : nq - 1;
+        }
+        const int rowa = f * kp.M + ma, rowb = f * kp.M + mb;
         // byte planes (stage_mf): sample n's high byte at byte 2 padw + n of
         // plane 0, its offset low byte at the same byte of plane 1
         const char *ra = reinterpret_cast<const char *>(sm.X + rowa * RS) + 2 * kp.PADW;
@@ -635,7 +660,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
                 al[d] = (int)__builtin_amdgcn_alignbyte(ul[d + 1], ul[d], sh);
             }
             // B: samples 64 beta + 16 (g + n - n0) .. + 15: one aligned 16-B read per plane
-            const int qb = 64 * beta + 16 * (g + rr - n0);
+            const int qb = 64 * beta + 16 * (g + cb - n0);
             const v4i_mf bh = *reinterpret_cast<const v4i_mf *>(rb + qb);
             const v4i_mf bl = *reinterpret_cast<const v4i_mf *>(rb + PLB + qb);
             hh = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bh, hh, 0, 0, 0);
@@ -643,16 +668,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(EMA &
             xx = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bh, xx, 0, 0, 0);
             ll = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bl, ll, 0, 0, 0);
         }
-        if (r < nq) {
-            // 128 (sum a + sum_window b) - 128^2 L; the b window starts at 16 (r - n0)
-            const int d = r - n0;
+        if (valid) {
+            // 128 (sum a + sum_window b) - 128^2 L; the b window starts at 16 (cb - n0)
+            const int d = cb - n0;
             const int sb = rsum[4 * rowb] - (d > 0 ? rsum[4 * rowb + d] : 0);
             const int64_t corr = 128 * ((int64_t)rsum[4 * rowa] + sb) - (int64_t)16384 * 64 * NB;
             int64_t *dst = sm.scores + sidx<KEYGRID>(f, p, S, P, K);
             constexpr int KS = KEYGRID ? 4 : 1;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                const int sl = 16 * (r - n0) + 4 * g + e;
+                const int sl = 16 * d + 4 * g + e;
                 if (sl >= -S && sl <= S)
                     dst[KS * sl] = (int64_t)hh[e] * 65536 + (int64_t)xx[e] * 256 + (int64_t)ll[e] + corr;
             }
@@ -941,6 +966,12 @@ int tdoa_launch_direct(const tdoa_kparams &kp_in, const tdoa_kout &out, const in
     if (tdoa_direct_fused_grid(kp)) {
         const int n0 = (kp.S + 15) / 16, nq = n0 + (kp.S + 1 + 15) / 16;  // lag columns -16 n0 .. 16 (nq - n0) - 1
         kp.PADW = MF_PADW;
+        // (frame, first mic) xcorr units at three mics (k_direct_mfma); TDOA_DIRECT_XC3=0: one unit per pair
+        static const bool xc3_off = [] {
+            const char *e = getenv("TDOA_DIRECT_XC3");
+            return e && e[0] == '0';
+        }();
+        kp.xc3 = kp.M == 3 && 2 * nq <= 16 && !xc3_off ? 1 : 0;
         kp.RS = kp.N / 2 + 2 * MF_PADW;
         int chunks = 0;
         mf_shape(kp, kp.F, threads, chunks, ema != nullptr);

@@ -80,6 +80,8 @@ struct tdoa_kparams {
     int32_t RS;      // staged row stride in words = N/2 + 2*PADW
     int32_t F;       // frames per workgroup
     int32_t TW;      // tuple words per lag tuple = ceil(P/4)
+    int32_t xc3;     // k_direct_mfma, three mics: a workgroup's xcorr units are (frame, first mic), the
+                     // partners' lag columns side by side in one MFMA tile (0: one unit per pair)
     uint8_t pair_i[TDOA_MAX_PAIRS];
     uint8_t pair_j[TDOA_MAX_PAIRS];
     // device tables
