@@ -10,6 +10,9 @@ switches once per process -- against the same oracles as the defaults:
   TDOA_EMA_WAVES=12  the 12-wave streaming DIRECT + EMA workgroup (config 5):
                      bit-exact against the oracle's sample-by-sample
                      sample_compute.h:53-146 (test_gpu_stream.py's compare)
+  TDOA_DIRECT_XC3=0  DIRECT's xcorr one MFMA tile per pair instead of per
+                     (frame, first mic) at three mics: config 2's batch bit-exact
+                     against the oracle, and the streaming run above
 
 The frame16 switches are tests/test_gpu_frame16_variants.py; TDOA_NO_COMPACT
 is tests/test_gpu_bench_path.py.  k_p1k_w64 measured slower and is built only
@@ -80,6 +83,24 @@ print("variant ok streaming")
 """
 
 
+XC3_OFF = r"""
+import numpy as np
+import oracle as O
+if not __import__("os").path.exists(O.LIB_PATH):
+    O.build()
+from tdoa import synth
+from tdoa.localizer import Localizer
+loc3 = Localizer()
+lut = loc3.lut().reshape(3, 101, 101)
+for B, seed in ((4096, synth.SEEDS[2]), (33, 1033)):
+    fr, _, _ = synth.adc_frames(B, 3, 1024, lut, 46, seed, device="cuda")
+    got = {k: v.cpu().numpy() for k, v in loc3.localize(fr, scores=True).items()}
+    exp = O.localize_batch(fr.cpu().numpy(), 46, loc3.window(), lut, threads=8)
+    for k in ("lags", "gate", "cell", "max_L", "xy", "scores", "weighted"):
+        assert np.array_equal(got[k], exp[k]), k
+""" + EMA12.replace('print("variant ok streaming")', 'print("variant ok xc3 off")')
+
+
 def _child(code, env):
     pre = f"import sys\nsys.path[:0] = {PATHS!r}\n"
     r = subprocess.run([sys.executable, "-c", pre + code], env=dict(os.environ, **env), capture_output=True,
@@ -95,3 +116,7 @@ def test_p1k_w64_vs_fp64_and_exhaustive_grid():
 
 def test_ema_waves_12_stream_bit_exact():
     _child(EMA12, {"TDOA_EMA_WAVES": "12"})
+
+
+def test_direct_xc3_off_bit_exact():
+    _child(XC3_OFF, {"TDOA_DIRECT_XC3": "0"})
