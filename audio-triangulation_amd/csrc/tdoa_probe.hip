@@ -71,7 +71,7 @@ extern "C" int tdoa_gpu_clock_mhz(int device, void *stream, double ms, double *m
     float *d_sink = nullptr;
     if (hipMalloc(&d_out, sizeof(unsigned long long) * 2 * waves) != hipSuccess ||
         hipMalloc(&d_sink, sizeof(float) * PROBE_THREADS) != hipSuccess) {
-        hipFree(d_out);
+        (void)hipFree(d_out);
         return tdoa_set_error(-2, "tdoa_gpu_clock_mhz: hipMalloc failed");
     }
     hipStream_t st = (hipStream_t)stream;
@@ -84,8 +84,8 @@ extern "C" int tdoa_gpu_clock_mhz(int device, void *stream, double ms, double *m
         e = hipMemcpyAsync(h.data(), d_out, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess)
         e = hipStreamSynchronize(st);
-    hipFree(d_out);
-    hipFree(d_sink);
+    (void)hipFree(d_out);
+    (void)hipFree(d_sink);
     if (e != hipSuccess)
         return tdoa_set_error(-2, "tdoa_gpu_clock_mhz: probe launch failed");
     std::vector<double> f;
