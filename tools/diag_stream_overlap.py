@@ -5,7 +5,10 @@ alternately, against one pipeline alone: the pair's time per hop-pair vs twice
 one pipeline's hop.  An upper bound on what overlapping hop h's DIRECT with hop
 h + 1's trigger inside one pipeline could gain.  Diagnostic only.
 
-    python tools/diag_stream_overlap.py [S] [hops]
+    python tools/diag_stream_overlap.py [S] [hops] [S_half]
+
+With S_half: also one pipeline of S streams against two of S_half each
+(the same streams as two shards on two HIP streams).
 """
 import os
 import sys
@@ -46,5 +49,15 @@ for rnd in range(3):
     two = run(pipes, K)
     print(f"round {rnd}: one pipeline {one * 1e6:.2f} us per hop; two pipelines {two * 1e6:.2f} us per hop pair "
           f"({two / 2 * 1e6:.2f} per hop, {100 * (1 - two / (2 * one)):.1f} % saved)")
+if len(sys.argv) > 3:
+    Sh = int(sys.argv[3])
+    halves = [StreamPipeline(loc, caps[0][i * Sh:(i + 1) * Sh].contiguous(), hop=H) for i in range(2)]
+    for rnd in range(3):
+        one = run(pipes[:1], K)
+        two = run(halves, K)
+        print(f"round {rnd}: {S} streams as one pipeline {one * 1e6:.2f} us per hop; as two shards of {Sh} "
+              f"{two * 1e6:.2f} us per hop")
+    for p in halves:
+        p.close()
 for p in pipes:
     p.close()
