@@ -106,7 +106,7 @@ def gpu_clock_mhz(dev, stream):
     return round(mhz.value, 1) if rc == 0 else None
 
 
-def settle(launches, R, dev, stream, max_s):
+def settle(launches, R, dev, stream, max_s, join=None):
     """Untimed windows of launches (max(R, 8) each: every rotating batch) until two
     consecutive windows' mean launch time (HIP events on the launch stream) agree
     within 2 %, or max_s has passed.  Returns the windows' means (us) and whether
@@ -119,6 +119,8 @@ def settle(launches, R, dev, stream, max_s):
         e0.record(stream)
         for k in range(n):
             launches[k % R]()
+        if join:
+            join()
         e1.record(stream)
         torch.cuda.synchronize(dev)
         means.append(e0.elapsed_time(e1) * 1e3 / n)
@@ -158,6 +160,9 @@ def parse():
                     help="longest the preflight waits for a steady launch time (configs 2-4)")
     ap.add_argument("--stream-graph", action="store_true",
                     help="config 5: replay each hop as a hipGraph (default: plain stream launches, faster)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="configs 2-4: consecutive steps alternate over this many HIP streams, own outputs each "
+                         "(0: 2 where a launch keeps no context scratch, else 1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: rehearse the N-process launch, rank logic and JSON line over gloo "
@@ -275,14 +280,26 @@ def time_engine(engine, args, dev, ri, cache):
         taus.append(tau)
     # config 4 is "28 pairs + least-squares": the LS refinement runs in the timed region
     ls = args.config == 4 and not args.no_grid
-    out = loc.alloc_outputs(B, grid=not args.no_grid, ls=ls)
-    stream = torch.cuda.current_stream(dev)
+    # consecutive steps alternate over Q HIP streams, each with its own output
+    # buffers: independent batches, so the next batch's waves start on the CUs
+    # the previous one has released instead of waiting for its slowest XCD
+    # (config 2: 27.1 vs 29.7 us per 4096-frame step, same box).  Only where a
+    # launch keeps no context scratch (the grid solved inside the transform
+    # kernel, no least squares): configs 3 / 4's k_grid_bb reads a per-context
+    # scratch that concurrent launches would share
+    safe = loc.batch_grid_fused() and not ls
+    Q = (2 if safe else 1) if args.streams <= 0 else (args.streams if safe else 1)
+    outs = [loc.alloc_outputs(B, grid=not args.no_grid, ls=ls) for _ in range(Q)]
+    out = outs[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(Q - 1)]
+    stream = streams[0]
     # preflight (untimed, before the W warmups): every rotating batch once, then
     # until preflight_s has passed (bounded); reported in the line
     # each rotating batch's launch prebuilt (Localizer.prepare: the same
     # tdoa_localize_batch as localize_into, its argument checks and ctypes
     # structs made once), so the timed loop's host Python is one C call per step
-    launches = [loc.prepare(batches[r], out, stream) for r in range(R)]
+    launches = [loc.prepare(batches[k % R], outs[k % Q], streams[k % Q]) for k in range(R * Q)]
+    R = R * Q
     pre_n, pre_t0 = 0, time.perf_counter()
     while args.preflight_s > 0 and (pre_n < R or time.perf_counter() - pre_t0 < args.preflight_s) \
             and pre_n < 20000:
@@ -291,12 +308,25 @@ def time_engine(engine, args, dev, ri, cache):
         if pre_n % 64 == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
-    steady = settle(launches, R, dev, stream, args.settle_max_s) if args.preflight_s > 0 else None
+    joins = [torch.cuda.Event() for _ in streams[1:]]
+
+    def join():  # the launch stream after every step stream's launches
+        for e, st in zip(joins, streams[1:]):
+            e.record(st)
+            stream.wait_event(e)
+
+    steady = settle(launches, R, dev, stream, args.settle_max_s, join) if args.preflight_s > 0 else None
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+
+    def start():  # every step stream after the event (the first steps of each)
+        ev0.record(stream)
+        for st in streams[1:]:
+            st.wait_event(ev0)
+
     t = shard.timed(lambda k: launches[k % R](), args.steps,
                     args.warmup, sync=lambda: torch.cuda.synchronize(dev), device=dev,
-                    on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+                    on_start=start, on_end=lambda: (join(), ev1.record(stream)))
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # GPU time per launch, launch stream
     clock = gpu_clock_mhz(dev, stream)
     total = shard.sum_over_ranks([B * args.steps], device=dev)[0]
@@ -313,7 +343,8 @@ def time_engine(engine, args, dev, ri, cache):
         "bytes_per_loc": bytes_per_loc,
         "achieved_gbs": bytes_per_loc * B / kern_s / 1e9,
         "valu_tflops": phat_flops(M, N) * B / kern_s / 1e12,
-        "rotate_batches": R,
+        "rotate_batches": R // Q,
+        "streams": Q,
         "preflight_steps": pre_n,
         "steady": steady,
         "ls": ls,
@@ -791,6 +822,7 @@ def main():
                        "engine": args.engine, "batch_per_gpu": B,
                        "global_batch": args.batch if cfg["scaling"] == "strong" else B * world,
                        "mics": cfg["M"], "frame_len": cfg["N"],
+                       "step_streams": main_res["streams"],
                        "parallelism": f"dp{world} (frame shards, no collective)"},
             "roofline": {"bound": "hbm", "achieved": main_res["achieved_gbs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
