@@ -834,6 +834,10 @@ def main():
                                                    main_res.get("grid_fused", True))
                          or "all kernels of a launch",
                          "kernel_ms": main_res["kernel_ms"],
+                         # step_streams > 1: kernel_ms is the events' span per step with that many
+                         # launches in flight; a profiler's per-dispatch duration spans the overlap
+                         # (one stream: the two agree, profiles/r06_c2_gcc_phat_kernel_stats_1stream.csv)
+                         "concurrent_launches": main_res["streams"],
                          "bytes_per_loc": main_res["bytes_per_loc"]},
             # the bound that actually binds an fp32 FFT path: FP32 vector issue
             "valu_roofline": _valu_roofline(args, main_res) if args.engine == "gcc_phat" else None,
