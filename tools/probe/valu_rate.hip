@@ -14,8 +14,10 @@ __global__ void __launch_bounds__(1024) k_rate(float *out, unsigned long long *c
     f2 a[C];
     float s[C];
     int u[C];
+    long long q[C];
 #pragma unroll
     for (int i = 0; i < C; i++) {
+        q[i] = (long long)t * (i + 3);
         a[i] = f2{(float)(t + i), (float)(t - i)};
         s[i] = (float)(t * i);
         u[i] = t + i;
@@ -50,6 +52,19 @@ __global__ void __launch_bounds__(1024) k_rate(float *out, unsigned long long *c
                     asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(u[i]) : "v"(t), "v"(u[(i + 1) % C]));
                 else if (KIND == 8)  // complex product by an SGPR constant (the c_mul_s pair)
                     asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel_hi:[0,1]\n\tv_pk_fma_f32 %0, %0, %1, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "+v"(a[i]) : "s"(m));
+                else if (KIND == 12) {  // 64-bit multiply-add of 32-bit operands
+                    unsigned long long cy;
+                    asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(q[i]), "=s"(cy) : "v"(t), "v"(u[i]));
+                } else if (KIND == 13)
+                    asm volatile("v_mad_i32_i24 %0, %0, %1, %2" : "+v"(u[i]) : "v"(t), "v"(u[(i + 1) % C]));
+                else if (KIND == 14)
+                    asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(t));
+                else if (KIND == 15)
+                    asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[i]) : "v"(q[(i + 1) % C]));
+                else if (KIND == 16) {  // 64-bit compare (VCC)
+                    asm volatile("v_cmp_gt_i64_e32 vcc, %0, %1" : : "v"(q[i]), "v"(q[(i + 1) % C]) : "vcc");
+                } else if (KIND == 17)
+                    asm volatile("v_lshlrev_b64 %0, 9, %0" : "+v"(q[i]));
                 else  // a VALU op followed by s_nop 0 (the inline-asm boundary padding)
                     asm volatile("v_pk_add_f32 %0, %0, %1\n\ts_nop 0" : "+v"(a[i]) : "v"(c));
             }
@@ -58,7 +73,7 @@ __global__ void __launch_bounds__(1024) k_rate(float *out, unsigned long long *c
     float acc = 0;
 #pragma unroll
     for (int i = 0; i < C; i++)
-        acc += a[i].x + a[i].y + s[i] + (float)u[i];
+        acc += a[i].x + a[i].y + s[i] + (float)u[i] + (float)q[i];
     out[blockIdx.x * blockDim.x + t] = acc;
     if ((t & 63) == 0)
         cyc[blockIdx.x * 16 + (t >> 6)] = t1 - t0;
@@ -92,6 +107,14 @@ int main()
     unsigned long long *cyc;
     (void)hipMalloc(&out, sizeof(float) * cus * 1024);
     (void)hipMalloc(&cyc, sizeof(unsigned long long) * cus * 16);
+    run<3, 16>(cus, out, cyc, "v_add_u32");
+    run<12, 16>(cus, out, cyc, "v_mad_i64_i32");
+    run<13, 16>(cus, out, cyc, "v_mad_i32_i24");
+    run<14, 16>(cus, out, cyc, "v_mul_lo_u32");
+    run<15, 16>(cus, out, cyc, "v_lshl_add_u64");
+    run<16, 16>(cus, out, cyc, "v_cmp_gt_i64");
+    run<17, 16>(cus, out, cyc, "v_lshlrev_b64");
+    return 0;
     run<0, 1>(cus, out, cyc, "v_pk_fma_f32");
     run<0, 4>(cus, out, cyc, "v_pk_fma_f32");
     run<0, 16>(cus, out, cyc, "v_pk_fma_f32");
