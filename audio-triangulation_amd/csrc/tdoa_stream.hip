@@ -218,6 +218,32 @@ __device__ __forceinline__ int wave_scan_incl(int v)
     return v;
 }
 
+// the same over several independent values, stage by stage: the values
+// interleave, so no DPP read follows the write of its own source (each such
+// pair costs an s_nop 1)
+template <int NV>
+__device__ __forceinline__ void wave_scan_incl_n(int (&v)[NV])
+{
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x111, 0xF, 0xF, false);  // row_shr:1
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x112, 0xF, 0xF, false);  // row_shr:2
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x114, 0xF, 0xF, false);  // row_shr:4
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x118, 0xF, 0xF, false);  // row_shr:8
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x142, 0xA, 0xF, false);  // row_bcast:15
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        v[j] += __builtin_amdgcn_update_dpp(0, v[j], 0x143, 0xC, 0xF, false);  // row_bcast:31
+}
+
 // Persistent: each wave walks streams gw, gw + GW, ... with the NEXT stream's
 // capture words and ring start already requested while it scans the current one
 // (a one-stream-per-wave form waited on its loads at the start of every wave:
@@ -346,30 +372,35 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
 #pragma unroll
             for (int m = 0; m < M; m++)
                 tot1[m] = 0;
+            // (the row's M + 1 dot chains and scans interleaved: a dot or DPP
+            // read right after the write of its own source waits in s_nops)
 #pragma unroll
             for (int r = 0; r < 3; r++) {
-                uint32_t c2 = 0;
+                uint32_t c[M + 1] = {};  // [0, M): mic m's samples, [M]: all squares
 #pragma unroll
-                for (int k = 0; k < CW; k++)
-                    c2 = __builtin_amdgcn_udot4(x[r][k], x[r][k], c2, false);
+                for (int k = 0; k < CW; k++) {
 #pragma unroll
-                for (int m = 0; m < M; m++) {
-                    uint32_t c1 = 0;
-#pragma unroll
-                    for (int k = 0; k < CW; k++) {
+                    for (int m = 0; m < M; m++) {
                         uint32_t mask = 0;  // bytes 4k + j of the chunk that are mic m's
 #pragma unroll
                         for (int j = 0; j < 4; j++)
                             mask |= ((4 * k + j) % M == m ? 1u : 0u) << (8 * j);
-                        c1 = __builtin_amdgcn_udot4(x[r][k], mask, c1, false);
+                        c[m] = __builtin_amdgcn_udot4(x[r][k], mask, c[m], false);
                     }
-                    const int inc = wave_scan_incl((int)c1);
-                    q1[r][m] = tot1[m] + inc - (int)c1;
-                    tot1[m] += __builtin_amdgcn_readlane(inc, 63);
+                    c[M] = __builtin_amdgcn_udot4(x[r][k], x[r][k], c[M], false);
                 }
-                const int inc2 = wave_scan_incl((int)c2);
-                q2[r] = tot2 + inc2 - (int)c2;
-                tot2 += __builtin_amdgcn_readlane(inc2, 63);
+                int inc[M + 1];
+#pragma unroll
+                for (int j = 0; j <= M; j++)
+                    inc[j] = (int)c[j];
+                wave_scan_incl_n(inc);
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    q1[r][m] = tot1[m] + inc[m] - (int)c[m];
+                    tot1[m] += __builtin_amdgcn_readlane(inc[m], 63);
+                }
+                q2[r] = tot2 + inc[M] - (int)c[M];
+                tot2 += __builtin_amdgcn_readlane(inc[M], 63);
             }
         }
         // the words re-enter here opaque: the scan re-extracts the samples
@@ -380,6 +411,8 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
             for (int k = 0; k < CW; k++)
                 asm volatile("" : "+v"(x[r][k]));
         const int64_t amin = rs + N - pos - 1;  // full ring: >= N samples since the last trigger
+        // (clamped to the candidates' range: a 32-bit compare per candidate)
+        const int amin32 = (int)(amin < 0 ? 0 : (amin > H ? H : amin));
         // the trigger of sample_compute.h:75-91 in difference form: with the
         // older / newer half-window sums so, si per mic and D2 = (q2[1] - q2[0])
         // - (q2[2] - q2[1]) of the squares, pout - pin = (D2 << hb) -
@@ -404,23 +437,37 @@ __global__ void __launch_bounds__(64 * TRIG_NWB) k_stream_trigger_p(tdoa_stream_
                 for (int k = (i * M) >> 2; k <= (i * M + M - 1) >> 2; k++)
                     asm volatile("" : "+v"(x[r][k]));
             const int a = G * lane + i;
+            // (accumulated by 64-bit multiply-adds from the squares' term: no
+            // 64-bit subtract and its carry chain)
             long long T = (long long)D2 << hb;
 #pragma unroll
             for (int m = 0; m < M; m++)
-                T -= (long long)(so[m] - si[m]) * (long long)(so[m] + si[m]);
-            if (fi < 0 && a >= amin && T > thr)
+                T += (long long)(si[m] - so[m]) * (long long)(so[m] + si[m]);
+            if (fi < 0 && a >= amin32 && T > thr)
                 fi = i;
-            int w0 = 0, w1 = 0, w2 = 0;
 #pragma unroll
             for (int m = 0; m < M; m++) {
                 const int v0 = smp(0, i, m), v1 = smp(1, i, m), v2 = smp(2, i, m);
                 so[m] += v1 - v0;
                 si[m] += v2 - v1;
-                w0 += v0 * v0;
-                w1 += v1 * v1;
-                w2 += v2 * v2;
             }
-            D2 += (w1 - w0) - (w2 - w1);
+            // sample i's squares summed over the mics, per row: its M bytes
+            // gathered into one word (v_perm, zeros above) and dotted with
+            // themselves -- two instructions a row (the compiler's form was a
+            // 24-bit multiply, a perm and a dot)
+            int w[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const int b = i * M, k = b >> 2, sh = b & 3;
+                uint32_t sel = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    sel |= (uint32_t)(j < M ? sh + j : 0x0C) << (8 * j);
+                const uint32_t hi = sh + M - 1 > 3 ? x[r][k + 1 < CW ? k + 1 : k] : x[r][k];
+                const uint32_t p = M == 4 ? x[r][k] : __builtin_amdgcn_perm(hi, x[r][k], sel);
+                w[r] = (int)__builtin_amdgcn_udot4(p, p, 0u, false);
+            }
+            D2 += (w[1] - w[0]) - (w[2] - w[1]);
         }
         const uint64_t fire = have ? __ballot(fi >= 0) : 0;
         if (fire != 0) {
