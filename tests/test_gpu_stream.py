@@ -126,12 +126,14 @@ def test_stream_reference_trace_fixture(loc48, oracle):
                 assert r["cell"] == g["orc_cell"][s, i]
 
 
-@pytest.mark.parametrize("N,hop,M", [(512, 256, 3), (2048, 1024, 3), (1024, 512, 4)])
+@pytest.mark.parametrize("N,hop,M", [(512, 256, 3), (2048, 1024, 3), (1024, 512, 4), (1024, 512, 2)])
 def test_stream_register_trigger_shapes(oracle, N, hop, M):
-    """frame_len = 2 x hop runs the register trigger scan (k_stream_trigger_w)
+    """frame_len = 2 x hop runs the register trigger scan (k_stream_trigger_p)
     for each (G = hop/64, M) it is instantiated for; config 5 is N 1024 / hop 512
-    / 3 mics (test_stream_vs_oracle)."""
-    mics = synth.square_mics(0.15) if M == 4 else None
+    / 3 mics (test_stream_vs_oracle).  M = 2: a sample's two bytes gathered by
+    the squares' v_perm (zeros above), M = 4: the word itself."""
+    mics = {4: synth.square_mics(0.15),
+            2: np.array([[-0.066, 0], [0.066, 0]], np.float32)}.get(M)
     loc = Localizer(sample_rate_hz=48000, frame_len=N, num_mics=M, mic_xy=mics)
     lut = loc.lut()
     T = (12 * N // hop) * hop
