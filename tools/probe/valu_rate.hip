@@ -107,6 +107,12 @@ int main()
     unsigned long long *cyc;
     (void)hipMalloc(&out, sizeof(float) * cus * 1024);
     (void)hipMalloc(&cyc, sizeof(unsigned long long) * cus * 16);
+    run<0, 16>(cus, out, cyc, "v_pk_fma_f32");
+    run<18, 16>(cus, out, cyc, "pk_fma+s_mov");
+    run<19, 16>(cus, out, cyc, "2pk_fma+s_mov");
+    run<20, 16>(cus, out, cyc, "pk_fma sgpr");
+    run<2, 16>(cus, out, cyc, "v_fma_f32");
+    return 0;
     run<3, 16>(cus, out, cyc, "v_add_u32");
     run<12, 16>(cus, out, cyc, "v_mad_i64_i32");
     run<13, 16>(cus, out, cyc, "v_mad_i32_i24");
